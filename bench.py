@@ -1,0 +1,201 @@
+#!/usr/bin/env python
+"""Benchmark of the APPNP propagation hot path on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload products-synth]
+
+A "step" is one full propagation call -- K=10 fused SpMM+AXPBY iterations over the whole
+graph (appnp_propagate, or the row-partitioned multi-GPU loop) -- on synthetic input that is
+resident in HBM before the timed region.  value = nodes * F * K * steps / time (whole job).
+
+N > 1 (launched by torch.distributed.run, one rank per GPU): the node set is row-partitioned
+across ranks and Z is RCCL all-gathered every iteration; the timed
+region is bracketed by barrier + synchronize and the max over ranks is reported.
+
+Extra JSON fields:
+  roofline      HBM roofline of the dominant kernel (k_step_*): algorithmic bytes per launch
+                B_iter = 4(N+1) + 8 nnz(A_hat) + 3 N F s   / average
+                launch time, measured with HIP events on the launch stream; peak 8 TB/s.
+  cpu_baseline  the oracle's torch.sparse.mm CPU loop (oracle/ppnp_oracle.py) on the same graph
+                and H, a bounded number of iterations, rank 0 at N=1 only.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "APPNP K=10 propagated node-feats/sec; achieved HBM GB/s vs peak, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip-level parameters)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--workload", default="products-synth")
+    p.add_argument("--cpu-iters", type=int, default=2,
+                   help="iterations of the CPU baseline sample (0 disables it)")
+    p.add_argument("--dist-mode", default="row", choices=["row", "row-overlap"])
+    return p.parse_args()
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(graph, H, K, alpha, iters):
+    """Time the oracle's CPU torch.sparse.mm APPNP loop on the same operator and H."""
+    from oracle import ppnp_oracle as O
+
+    rp, col, val, _ = graph.csr()
+    a_t = torch.sparse_csr_tensor(rp.cpu().long(), col.cpu().long(), val.cpu(),
+                                  size=(graph.n, graph.n))
+    Hc = H.float().cpu()
+    threads = torch.get_num_threads()
+    t0 = time.perf_counter()
+    O.appnp_propagate_torch_cpu(a_t, Hc, iters, alpha)
+    dt = time.perf_counter() - t0
+    n, f = Hc.shape
+    return {
+        "value": n * f * iters / dt,
+        "unit": "node-feats/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"full graph, {iters} of K={K} iterations, torch.sparse.mm fp32 CSR "
+                  f"(oracle/ppnp_oracle.py appnp_propagate_torch_cpu), {dt:.2f} s",
+    }
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+
+    import ppnp_amd
+    from ppnp_amd import synth
+
+    n, m, F, K, alpha, dtype = synth.CONFIGS[args.workload]
+    seed = synth.SEEDS.get(args.workload, 0)
+    t0 = time.perf_counter()
+    indptr, indices = synth.uniform_graph_device(n, m, seed, device=dev)
+    H = synth.features(n, F, dtype=dtype, device=dev)
+    torch.cuda.synchronize()
+    t_gen = time.perf_counter() - t0
+
+    if world > 1:
+        from ppnp_amd import dist as pdist
+
+        runner = pdist.RowPartitionAPPNP.create(indptr, indices, n, H, K, alpha, dev,
+                                                overlap=args.dist_mode == "row-overlap")
+        graph = runner.graph
+        run = runner.run
+        stream = torch.cuda.current_stream(dev)
+    else:
+        t1 = time.perf_counter()
+        graph = ppnp_amd.Graph.from_csr(indptr, indices, None, n, mode="sym", device=dev)
+        torch.cuda.synchronize()
+        t_build = time.perf_counter() - t1
+        Z = torch.empty_like(H)
+
+        def run():
+            ppnp_amd.propagate_forward(graph, H, K, alpha, out=Z)
+
+        stream = torch.cuda.current_stream(dev)
+    del indices
+    nnz_hat = graph.nnz_hat if world == 1 else runner.nnz_hat_total
+    if rank == 0:
+        log(f"[bench] {args.workload}: N={n} nnz_hat={nnz_hat} F={F} K={K} dtype={dtype} "
+            f"gen {t_gen:.2f}s" + (f" build {t_build:.3f}s" if world == 1 else ""))
+
+    for _ in range(args.warmup):
+        run()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        run()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    dev_ms = ev0.elapsed_time(ev1)
+    if world > 1:
+        t = torch.tensor([wall, dev_ms], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        wall, dev_ms = float(t[0]), float(t[1])
+
+    s = 2 if dtype == torch.bfloat16 else 4
+    rows_local = graph.rows
+    nnz_local = graph.nnz_hat
+    # dominant kernel: one SpMM launch per iteration per rank
+    b_iter = 4 * (rows_local + 1) + 8 * nnz_local + 3 * rows_local * F * s
+    avg_launch_ms = dev_ms / (args.steps * K)
+    achieved = b_iter / (avg_launch_ms * 1e-3) / 1e9
+    value = n * F * K * args.steps / wall
+    res = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "node-feats/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": wall * 1e3 / args.steps,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "bf16" if dtype == torch.bfloat16 else "f32",
+        "data": "synthetic (uniform random graph with the dataset's node/edge counts, "
+                "H ~ N(0,1))",
+        "config": {
+            "workload": args.workload,
+            "nodes": n,
+            "nnz_a_hat": nnz_hat,
+            "F": F,
+            "K": K,
+            "alpha": alpha,
+            "norm": "sym",
+            "parallelism": f"row{world}" if world > 1 else "single",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": None,
+            "kernel": "k_step_wide (one launch per iteration)",
+            "bytes_per_launch": b_iter,
+            "avg_launch_ms": avg_launch_ms,
+        },
+    }
+    if world == 1 and args.cpu_iters > 0:
+        res["cpu_baseline"] = cpu_baseline(graph, H, K, alpha, args.cpu_iters)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,148 @@
+/*
+ * ppnp_amd.h -- C ABI of the MI355X (gfx950) APPNP propagation path.
+ *
+ * This is the drop-in boundary for the propagation hot path of bkj/ppnp.  The reference
+ * has no FFI of its own (it is pure Python); each entry point below names the reference
+ * interface it replaces (file:line under the reference checkout):
+ *
+ *   appnp_graph_create*   helpers.py:58-66   calc_A_hat(adj, mode)   (host scipy, fp64)
+ *                         helpers.py:68-71   compute_ppr(...)         (dense O(N^3) inverse)
+ *   appnp_propagate       model.py:63        self.ppr[idx] @ self.encoder(X)  -- the dense
+ *                                            PPR product becomes K fused CSR SpMM+AXPBY
+ *                                            launches  Z <- (1-a) A_hat Z + a H
+ *   appnp_propagate_bwd   model.py:63        autograd of the same product (dH = J^T dZ)
+ *   appnp_step            one iteration; used by the row-partitioned multi-GPU driver
+ *
+ * Conventions
+ *   - Every function returns 0 (APPNP_OK) or a negative errno-style code; nothing throws or
+ *     aborts across the ABI.  appnp_strerror() names a code.
+ *   - All array arguments are DEVICE pointers on the current HIP device; the caller owns H,
+ *     Z, dZ, dH and the workspace; the graph handle owns its device CSR.
+ *   - `stream` is a hipStream_t passed as void* (NULL = the null stream).  appnp_propagate,
+ *     appnp_propagate_bwd and appnp_step are asynchronous and stream-ordered: no host sync,
+ *     no allocation (graph-capturable).  appnp_graph_create* allocates and synchronises.
+ *   - Dense matrices are row-major with a leading dimension `ld` in ELEMENTS (ld >= f).
+ *   - A handle is not thread-safe; distinct handles are independent.
+ */
+#ifndef PPNP_AMD_H
+#define PPNP_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PPNP_AMD_ABI_VERSION 1
+
+typedef struct appnp_graph appnp_graph;
+
+enum appnp_status {
+  APPNP_OK = 0,
+  APPNP_EDEVICE = -5,   /* HIP runtime / kernel launch failure            */
+  APPNP_ENOMEM = -12,   /* device allocation failed                       */
+  APPNP_EINVAL = -22,   /* bad argument (shape, pointer, ld, alignment)   */
+  APPNP_ERANGE = -34,   /* size exceeds the int32 CSR index range         */
+  APPNP_ENOTSUP = -95   /* valid request this build does not implement    */
+};
+
+/* helpers.py:61-66: 'sym' = D^-1/2 (A+I) D^-1/2, 'rw' = D^-1 (A+I) */
+enum appnp_norm { APPNP_NORM_SYM = 0, APPNP_NORM_RW = 1 };
+
+/* storage type of H / Z (accumulation is always fp32) */
+enum appnp_dtype { APPNP_F32 = 0, APPNP_BF16 = 1 };
+
+int appnp_abi_version(void);
+const char* appnp_strerror(int code);
+
+/*
+ * Build A_hat on the device from the CSR of A (helpers.py:58-66).
+ *   indptr[n+1], indices[nnz]: int32 CSR of A, columns strictly increasing in each row
+ *                              (scipy canonical form); device pointers.
+ *   vals[nnz]: fp32 edge weights, or NULL for an unweighted graph (all ones).
+ *   A may or may not contain diagonal entries: A+I merges them (a_ii + 1), exactly as
+ *   `adj + sp.eye(n)` does, and entries whose merged value is 0 are dropped.
+ * Degrees are fp64 weighted row sums of A+I; A_hat values are computed in fp64 and rounded
+ * once to fp32, so they equal float32(calc_A_hat(adj, mode).data) bit for bit.
+ */
+int appnp_graph_create(const int32_t* indptr, const int32_t* indices, const float* vals,
+                       int64_t n, int64_t nnz, int mode, void* stream, appnp_graph** out);
+
+/*
+ * Same, but keeps only rows [row_lo, row_hi) of A_hat (global column indices); degrees of
+ * all n nodes are still computed from the full A.  Used for the row-partitioned multi-GPU
+ * path: rank r owns rows [row_lo, row_hi).  With split_local != 0 the rows are also stored
+ * as two CSRs -- columns inside [row_lo,row_hi) ("local") and outside ("remote") -- so the
+ * local product can overlap the all-gather of the remote rows.
+ */
+int appnp_graph_create_rows(const int32_t* indptr, const int32_t* indices, const float* vals,
+                            int64_t n, int64_t nnz, int mode, int64_t row_lo, int64_t row_hi,
+                            int split_local, void* stream, appnp_graph** out);
+
+void appnp_graph_destroy(appnp_graph* g);
+
+/* n (global nodes), rows held [row_lo,row_hi), nnz of the held A_hat rows, symmetric flag
+ * (1 if A's pattern and weights are symmetric, so A_hat^T == A_hat for 'sym'). */
+int appnp_graph_info(const appnp_graph* g, int64_t* n, int64_t* row_lo, int64_t* row_hi,
+                     int64_t* nnz_hat, int* mode, int* symmetric);
+
+/* Read-only device views of the held A_hat CSR (row_ptr is local: row_ptr[0] == 0). */
+int appnp_graph_csr(const appnp_graph* g, const int32_t** row_ptr, const int32_t** col,
+                    const float** val);
+
+/* Stream-ordered copy of the held A_hat CSR and of dinv into caller-owned device buffers
+ * (row_ptr[rows+1], col[nnz_hat], val[nnz_hat], dinv[n]); any pointer may be NULL. */
+int appnp_graph_copy_csr(const appnp_graph* g, int32_t* row_ptr, int32_t* col, float* val,
+                         double* dinv, void* stream);
+
+/* Device view of the fp64 inverse-degree vector (1/sqrt(D) for sym, 1/D for rw), length n. */
+int appnp_graph_dinv(const appnp_graph* g, const double** dinv);
+
+/* Bytes of workspace appnp_propagate / appnp_propagate_bwd need for this shape. */
+size_t appnp_workspace_bytes(const appnp_graph* g, int64_t f, int64_t ld, int dtype);
+
+/*
+ * Z = APPNP_K(H):  Z_0 = H;  Z_{k+1} = (1-alpha) (M_k o A_hat) Z_k + alpha H,  k < K.
+ *   H, Z: n x f, leading dims ld_h / ld_z, `dtype` storage; must not alias.
+ *   p_drop in [0,1): edge dropout; M_k keeps edge (i,j) at step k iff the 24-bit counter
+ *   hash of (seed, k, i, j) >= p_drop * 2^24, and scales kept edges by 1/(1-p_drop).
+ *   p_drop = 0 is eval mode (the reference's semantics).
+ *   ws: appnp_workspace_bytes() bytes (may be NULL when that is 0).
+ * One fused kernel launch per iteration.  Requires a full (non-partitioned) graph.
+ */
+int appnp_propagate(const appnp_graph* g, const void* H, int64_t ld_h, void* Z, int64_t ld_z,
+                    int64_t f, int dtype, int K, float alpha, float p_drop, uint64_t seed,
+                    void* ws, size_t ws_bytes, void* stream);
+
+/*
+ * dH = J^T dZ for the map H -> Z of appnp_propagate with the same (K, alpha, p_drop, seed).
+ * Uses A_hat^T; supported when the graph is symmetric (sym mode on an undirected graph),
+ * APPNP_ENOTSUP otherwise.
+ */
+int appnp_propagate_bwd(const appnp_graph* g, const void* dZ, int64_t ld_dz, void* dH,
+                        int64_t ld_dh, int64_t f, int dtype, int K, float alpha, float p_drop,
+                        uint64_t seed, void* ws, size_t ws_bytes, void* stream);
+
+/*
+ * One iteration on the held rows:  Zout[i-row_lo] = (1-alpha) sum_j (M_k o A_hat)_ij Zin[j]
+ *                                                   + alpha H[i-row_lo],  i in [row_lo,row_hi)
+ *   Zin: all n rows (global row index), Zout/H: the held rows only.
+ *   part selects which stored CSR is applied:
+ *     APPNP_PART_ALL     the held rows' full CSR (epilogue as above)
+ *     APPNP_PART_LOCAL   local-column CSR only:  P[i] = (1-alpha) sum_local ...   (P = Zout, fp32)
+ *     APPNP_PART_REMOTE  remote-column CSR, finishing: Zout = (1-alpha) sum_remote + P + alpha H
+ *                        (P passed as `partial`, fp32, ld = ld_partial)
+ */
+enum appnp_part { APPNP_PART_ALL = 0, APPNP_PART_LOCAL = 1, APPNP_PART_REMOTE = 2 };
+
+int appnp_step(const appnp_graph* g, int part, const void* Zin, int64_t ld_in, const void* H,
+               int64_t ld_h, void* Zout, int64_t ld_out, const float* partial,
+               int64_t ld_partial, int64_t f, int dtype, int k, float alpha, float p_drop,
+               uint64_t seed, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PPNP_AMD_H */

@@ -1,0 +1,23 @@
+"""ppnp_amd -- MI355X (gfx950) APPNP propagation path for bkj/ppnp.
+
+The hot path: A_hat construction (helpers.py:58-66) and the APPNP
+propagation loop Z <- (1-a) A_hat Z + a H that replaces the dense PPR product of
+model.py:63, as hand-written HIP kernels behind the C ABI in include/ppnp_amd.h.
+"""
+
+from . import _lib
+from .graph import Graph
+from .model import APPNP, PPNP, CustomLinear
+from .ops import propagate, propagate_backward, propagate_forward, step
+
+__all__ = [
+    "APPNP",
+    "PPNP",
+    "CustomLinear",
+    "Graph",
+    "propagate",
+    "propagate_forward",
+    "propagate_backward",
+    "step",
+    "_lib",
+]

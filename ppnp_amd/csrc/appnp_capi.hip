@@ -1,0 +1,319 @@
+// appnp_capi.hip -- the extern "C" boundary declared in include/ppnp_amd.h.
+//
+// Argument validation, workspace ping-pong and the K-iteration launch sequence.  No host
+// synchronisation or allocation happens in appnp_propagate / appnp_propagate_bwd /
+// appnp_step, so a caller may capture them in a hipGraph.
+#include <new>
+
+#include "../../include/ppnp_amd.h"
+#include "appnp_internal.h"
+
+using appnp::StepArgs;
+
+namespace {
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+inline int dev_err(hipError_t e) {
+  if (e == hipSuccess) return APPNP_OK;
+  if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) return APPNP_ENOMEM;
+  if (e == hipErrorInvalidValue) return APPNP_EINVAL;
+  return APPNP_EDEVICE;
+}
+
+inline int64_t elem_size(int dtype) { return dtype == APPNP_F32 ? 4 : 2; }
+
+inline bool valid_dtype(int dtype) { return dtype == APPNP_F32 || dtype == APPNP_BF16; }
+
+// Per-iteration dropout parameters (identical to oracle/ppnp_oracle.py edge_keep_mask).
+void set_drop(StepArgs& a, float p_drop, uint64_t seed, int k) {
+  if (p_drop > 0.0f) {
+    a.mkey = appnp::splitmix64(seed + (uint64_t)(k + 1) * 0x9E3779B97F4A7C15ull);
+    double thr = (double)p_drop * (double)(1u << 24);
+    a.drop_thr = (uint32_t)thr;
+    if (a.drop_thr == 0u) a.drop_thr = 0u;
+    a.drop_scale = 1.0f / (1.0f - p_drop);
+  } else {
+    a.mkey = 0;
+    a.drop_thr = 0u;
+    a.drop_scale = 1.0f;
+  }
+}
+
+int check_common(const appnp_graph* g, int64_t f, int dtype, int K, float alpha, float p_drop) {
+  if (!g) return APPNP_EINVAL;
+  if (f < 0 || f > INT32_MAX || K < 0 || !valid_dtype(dtype)) return APPNP_EINVAL;
+  if (!(alpha >= 0.0f && alpha <= 1.0f)) return APPNP_EINVAL;
+  if (!(p_drop >= 0.0f && p_drop < 1.0f)) return APPNP_EINVAL;
+  return APPNP_OK;
+}
+
+StepArgs base_args(const appnp_graph* g, int64_t f, float alpha) {
+  StepArgs a{};
+  a.row_ptr = g->row_ptr;
+  a.col = g->col;
+  a.val = g->val;
+  a.n_rows = g->row_hi - g->row_lo;
+  a.row_lo = g->row_lo;
+  a.f = (int32_t)f;
+  a.scale = 1.0f - alpha;
+  a.alpha = alpha;
+  a.drop_scale = 1.0f;
+  return a;
+}
+
+}  // namespace
+
+extern "C" {
+
+int appnp_abi_version(void) { return PPNP_AMD_ABI_VERSION; }
+
+const char* appnp_strerror(int code) {
+  switch (code) {
+    case APPNP_OK: return "ok";
+    case APPNP_EDEVICE: return "HIP device error";
+    case APPNP_ENOMEM: return "out of device memory";
+    case APPNP_EINVAL: return "invalid argument";
+    case APPNP_ERANGE: return "size exceeds int32 CSR index range";
+    case APPNP_ENOTSUP: return "not supported";
+    default: return "unknown error";
+  }
+}
+
+int appnp_graph_create_rows(const int32_t* indptr, const int32_t* indices, const float* vals,
+                            int64_t n, int64_t nnz, int mode, int64_t row_lo, int64_t row_hi,
+                            int split_local, void* stream, appnp_graph** out) {
+  if (!out) return APPNP_EINVAL;
+  *out = nullptr;
+  if (n < 0 || nnz < 0 || n > INT32_MAX || nnz > INT32_MAX) return n > INT32_MAX || nnz > INT32_MAX ? APPNP_ERANGE : APPNP_EINVAL;
+  if (mode != APPNP_NORM_SYM && mode != APPNP_NORM_RW) return APPNP_EINVAL;
+  if (row_lo < 0 || row_hi < row_lo || row_hi > n) return APPNP_EINVAL;
+  if (n > 0 && !indptr) return APPNP_EINVAL;
+  if (nnz > 0 && !indices) return APPNP_EINVAL;
+  appnp_graph* g = new (std::nothrow) appnp_graph();
+  if (!g) return APPNP_ENOMEM;
+  const int rc = appnp::graph_build(indptr, indices, vals, n, nnz, mode, row_lo, row_hi,
+                                    split_local, as_stream(stream), g);
+  if (rc != APPNP_OK) {
+    delete g;
+    return rc;
+  }
+  *out = g;
+  return APPNP_OK;
+}
+
+int appnp_graph_create(const int32_t* indptr, const int32_t* indices, const float* vals,
+                       int64_t n, int64_t nnz, int mode, void* stream, appnp_graph** out) {
+  return appnp_graph_create_rows(indptr, indices, vals, n, nnz, mode, 0, n, 0, stream, out);
+}
+
+void appnp_graph_destroy(appnp_graph* g) {
+  if (!g) return;
+  appnp::graph_free(g);
+  delete g;
+}
+
+int appnp_graph_info(const appnp_graph* g, int64_t* n, int64_t* row_lo, int64_t* row_hi,
+                     int64_t* nnz_hat, int* mode, int* symmetric) {
+  if (!g) return APPNP_EINVAL;
+  if (n) *n = g->n;
+  if (row_lo) *row_lo = g->row_lo;
+  if (row_hi) *row_hi = g->row_hi;
+  if (nnz_hat) *nnz_hat = g->nnz_hat;
+  if (mode) *mode = g->mode;
+  if (symmetric) *symmetric = g->symmetric;
+  return APPNP_OK;
+}
+
+int appnp_graph_csr(const appnp_graph* g, const int32_t** row_ptr, const int32_t** col,
+                    const float** val) {
+  if (!g) return APPNP_EINVAL;
+  if (row_ptr) *row_ptr = g->row_ptr;
+  if (col) *col = g->col;
+  if (val) *val = g->val;
+  return APPNP_OK;
+}
+
+int appnp_graph_copy_csr(const appnp_graph* g, int32_t* row_ptr, int32_t* col, float* val,
+                         double* dinv, void* stream) {
+  if (!g) return APPNP_EINVAL;
+  const hipStream_t s = as_stream(stream);
+  const int64_t rows = g->row_hi - g->row_lo;
+  hipError_t e = hipSuccess;
+  if (row_ptr && e == hipSuccess)
+    e = hipMemcpyAsync(row_ptr, g->row_ptr, (rows + 1) * sizeof(int32_t), hipMemcpyDeviceToDevice, s);
+  if (col && g->nnz_hat && e == hipSuccess)
+    e = hipMemcpyAsync(col, g->col, g->nnz_hat * sizeof(int32_t), hipMemcpyDeviceToDevice, s);
+  if (val && g->nnz_hat && e == hipSuccess)
+    e = hipMemcpyAsync(val, g->val, g->nnz_hat * sizeof(float), hipMemcpyDeviceToDevice, s);
+  if (dinv && g->n && e == hipSuccess)
+    e = hipMemcpyAsync(dinv, g->dinv, g->n * sizeof(double), hipMemcpyDeviceToDevice, s);
+  return dev_err(e);
+}
+
+int appnp_graph_dinv(const appnp_graph* g, const double** dinv) {
+  if (!g || !dinv) return APPNP_EINVAL;
+  *dinv = g->dinv;
+  return APPNP_OK;
+}
+
+size_t appnp_workspace_bytes(const appnp_graph* g, int64_t f, int64_t ld, int dtype) {
+  if (!g || f < 0 || !valid_dtype(dtype)) return 0;
+  if (ld < f) ld = f;
+  const int64_t rows = g->row_hi - g->row_lo;
+  // two ping-pong buffers (the forward needs one, the adjoint two)
+  return (size_t)(2 * rows * ld * elem_size(dtype));
+}
+
+int appnp_propagate(const appnp_graph* g, const void* H, int64_t ld_h, void* Z, int64_t ld_z,
+                    int64_t f, int dtype, int K, float alpha, float p_drop, uint64_t seed,
+                    void* ws, size_t ws_bytes, void* stream) {
+  int rc = check_common(g, f, dtype, K, alpha, p_drop);
+  if (rc) return rc;
+  if (g->row_lo != 0 || g->row_hi != g->n) return APPNP_EINVAL;  // needs the whole graph
+  const int64_t n = g->n;
+  if (n == 0 || f == 0) return APPNP_OK;
+  if (!H || !Z || ld_h < f || ld_z < f || H == Z) return APPNP_EINVAL;
+  const hipStream_t s = as_stream(stream);
+  const int64_t es = elem_size(dtype);
+  if (K == 0)
+    return dev_err(hipMemcpy2DAsync(Z, ld_z * es, H, ld_h * es, f * es, n,
+                                    hipMemcpyDeviceToDevice, s));
+  const int64_t ld_w = ld_z;
+  if (K >= 2) {
+    if (!ws || ws_bytes < (size_t)(n * ld_w * es)) return APPNP_EINVAL;
+  }
+  const int64_t lds[3] = {ld_h, ld_z, ld_w};
+  const void* ptrs[3] = {H, Z, K >= 2 ? ws : nullptr};
+  const int V = appnp::pick_vec(dtype, f, lds, 3, ptrs, 3);
+
+  StepArgs a = base_args(g, f, alpha);
+  a.h = H;
+  a.ld_h = ld_h;
+  const void* src = H;
+  int64_t ld_src = ld_h;
+  for (int k = 0; k < K; ++k) {
+    // the last iteration must land in Z: alternate backwards from it
+    const bool to_z = ((K - 1 - k) % 2) == 0;
+    void* dst = to_z ? Z : ws;
+    const int64_t ld_dst = to_z ? ld_z : ld_w;
+    a.zin = src;
+    a.ld_in = ld_src;
+    a.out = dst;
+    a.ld_out = ld_dst;
+    set_drop(a, p_drop, seed, k);
+    rc = dev_err(appnp::launch_step(dtype, appnp::EPI_FWD, V, a, s));
+    if (rc) return rc;
+    src = dst;
+    ld_src = ld_dst;
+  }
+  return APPNP_OK;
+}
+
+int appnp_propagate_bwd(const appnp_graph* g, const void* dZ, int64_t ld_dz, void* dH,
+                        int64_t ld_dh, int64_t f, int dtype, int K, float alpha, float p_drop,
+                        uint64_t seed, void* ws, size_t ws_bytes, void* stream) {
+  int rc = check_common(g, f, dtype, K, alpha, p_drop);
+  if (rc) return rc;
+  if (g->row_lo != 0 || g->row_hi != g->n) return APPNP_EINVAL;
+  // A_hat^T is only available as A_hat itself: symmetric 'sym' operator
+  if (!(g->mode == APPNP_NORM_SYM && g->symmetric)) return APPNP_ENOTSUP;
+  const int64_t n = g->n;
+  if (n == 0 || f == 0) return APPNP_OK;
+  if (!dZ || !dH || ld_dz < f || ld_dh < f || dZ == dH) return APPNP_EINVAL;
+  const hipStream_t s = as_stream(stream);
+  const int64_t es = elem_size(dtype);
+  if (K == 0)
+    return dev_err(hipMemcpy2DAsync(dH, ld_dh * es, dZ, ld_dz * es, f * es, n,
+                                    hipMemcpyDeviceToDevice, s));
+  const int64_t ld_w = ld_dh;
+  const int64_t buf = n * ld_w * es;
+  const int nbuf = K >= 3 ? 2 : (K == 2 ? 1 : 0);
+  if (nbuf > 0 && (!ws || ws_bytes < (size_t)(nbuf * buf))) return APPNP_EINVAL;
+  void* w0 = ws;
+  void* w1 = nbuf == 2 ? static_cast<char*>(ws) + buf : nullptr;
+  const int64_t lds[3] = {ld_dz, ld_dh, ld_w};
+  const void* ptrs[4] = {dZ, dH, w0, w1};
+  const int V = appnp::pick_vec(dtype, f, lds, 3, ptrs, 4);
+
+  // dH = alpha * dZ  (the k = K term), then G_k = (1-alpha) M_k^T G_{k+1},
+  // dH += alpha G_k (k >= 1) / dH += G_0.
+  rc = dev_err(appnp::launch_scale_rows(dtype, dZ, ld_dz, dH, ld_dh, n, f, alpha, s));
+  if (rc) return rc;
+  StepArgs a = base_args(g, f, alpha);
+  a.tkey = 1;
+  a.aux = dH;
+  a.ld_aux = ld_dh;
+  const void* src = dZ;
+  int64_t ld_src = ld_dz;
+  int flip = 0;
+  for (int k = K - 1; k >= 0; --k) {
+    void* dst = k == 0 ? nullptr : (flip ? w1 : w0);
+    a.zin = src;
+    a.ld_in = ld_src;
+    a.out = dst;
+    a.ld_out = ld_w;
+    a.alpha = k >= 1 ? alpha : 1.0f;
+    set_drop(a, p_drop, seed, k);
+    rc = dev_err(appnp::launch_step(dtype, appnp::EPI_BWD, V, a, s));
+    if (rc) return rc;
+    src = dst;
+    ld_src = ld_w;
+    flip ^= 1;
+  }
+  return APPNP_OK;
+}
+
+int appnp_step(const appnp_graph* g, int part, const void* Zin, int64_t ld_in, const void* H,
+               int64_t ld_h, void* Zout, int64_t ld_out, const float* partial,
+               int64_t ld_partial, int64_t f, int dtype, int k, float alpha, float p_drop,
+               uint64_t seed, void* stream) {
+  int rc = check_common(g, f, dtype, 0, alpha, p_drop);
+  if (rc) return rc;
+  if (k < 0) return APPNP_EINVAL;
+  const int64_t rows = g->row_hi - g->row_lo;
+  if (rows == 0 || f == 0) return APPNP_OK;
+  if (!Zin || !Zout || ld_in < f || ld_out < f) return APPNP_EINVAL;
+  StepArgs a = base_args(g, f, alpha);
+  a.zin = Zin;
+  a.ld_in = ld_in;
+  a.out = Zout;
+  a.ld_out = ld_out;
+  set_drop(a, p_drop, seed, k);
+  int epi = appnp::EPI_FWD;
+  int64_t lds[4] = {ld_in, ld_out, ld_h, ld_partial};
+  const void* ptrs[4] = {Zin, Zout, H, partial};
+  int n_ld = 2;
+  if (part == APPNP_PART_ALL) {
+    if (!H || ld_h < f) return APPNP_EINVAL;
+    a.h = H;
+    a.ld_h = ld_h;
+    n_ld = 3;
+  } else {
+    if (!g->split) return APPNP_EINVAL;
+    if (dtype != APPNP_F32) return APPNP_ENOTSUP;
+    if (part == APPNP_PART_LOCAL) {
+      epi = appnp::EPI_PARTIAL;
+      a.row_ptr = g->lrow_ptr;
+      a.col = g->lcol;
+      a.val = g->lval;
+    } else if (part == APPNP_PART_REMOTE) {
+      if (!H || ld_h < f || !partial || ld_partial < f) return APPNP_EINVAL;
+      epi = appnp::EPI_FINISH;
+      a.row_ptr = g->rrow_ptr;
+      a.col = g->rcol;
+      a.val = g->rval;
+      a.h = H;
+      a.ld_h = ld_h;
+      a.aux = const_cast<float*>(partial);
+      a.ld_aux = ld_partial;
+      n_ld = 4;
+    } else {
+      return APPNP_EINVAL;
+    }
+  }
+  const int V = appnp::pick_vec(dtype, f, lds, n_ld, ptrs, 4);
+  return dev_err(appnp::launch_step(dtype, epi, V, a, as_stream(stream)));
+}
+
+}  // extern "C"

@@ -1,0 +1,142 @@
+// appnp_device.h -- shared device-side definitions for the gfx950 APPNP propagation path.
+//
+// Internal to libppnp_amd.so.  The public ABI is include/ppnp_amd.h.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace appnp {
+
+constexpr int kWave = 64;           // CDNA wavefront
+constexpr int kBlock = 256;         // 4 waves per workgroup
+constexpr int kWavesPerBlock = kBlock / kWave;
+
+// Epilogue of one propagation step (y = scale * sum_j w_ij Zin[j]):
+//   FWD      out = y + alpha * H                    (forward iteration)
+//   BWD      out = y (if out != null); aux += alpha * y   (adjoint iteration; aux = dH)
+//   PARTIAL  out(fp32) = y                          (local-column half of a split step)
+//   FINISH   out = y + aux(fp32) + alpha * H        (remote-column half of a split step)
+enum Epi { EPI_FWD = 0, EPI_BWD = 1, EPI_PARTIAL = 2, EPI_FINISH = 3 };
+
+struct StepArgs {
+  const int32_t* row_ptr;  // local rows, row_ptr[0] == 0
+  const int32_t* col;      // global column index
+  const float* val;        // A_hat values (fp32)
+  const void* zin;         // all n rows (global index)
+  const void* h;           // held rows (local index)
+  void* out;               // held rows (local index)
+  void* aux;               // BWD: dH (storage dtype); FINISH: fp32 partial
+  int64_t ld_in, ld_h, ld_out, ld_aux;
+  int64_t n_rows;          // rows held
+  int64_t row_lo;          // global index of local row 0 (hash key only)
+  uint64_t mkey;           // per-iteration dropout key = splitmix64(seed + (k+1)*golden)
+  int32_t f;               // features
+  uint32_t drop_thr;       // 24-bit drop threshold; 0 = no dropout
+  float scale;             // 1 - alpha
+  float alpha;             // weight of H (FWD/FINISH) or of y into aux (BWD)
+  float drop_scale;        // 1 / (1 - p)
+  int32_t tkey;            // 1: hash key of entry (row i, col j) is (j, i)  (transposed operator)
+};
+
+__host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+// Edge dropout: counter hash of (key, row, col); identical to oracle/ppnp_oracle.py
+// edge_keep_mask.  Independent of the partition and of the visiting order.
+__device__ __forceinline__ float edge_weight(float w, int64_t grow, int32_t c,
+                                             const StepArgs& a) {
+  if (a.drop_thr == 0u) return w;
+  const uint64_t r = (uint32_t)grow, cc = (uint32_t)c;
+  const uint64_t key = a.tkey ? ((cc << 32) | r) : ((r << 32) | cc);
+  const uint64_t h = splitmix64(key ^ a.mkey);
+  return ((uint32_t)(h >> 40) >= a.drop_thr) ? w * a.drop_scale : 0.0f;
+}
+
+// ---- storage traits: V consecutive elements <-> V fp32 registers -------------------------
+
+__device__ __forceinline__ float bf16_to_f32(uint32_t b) { return __uint_as_float(b << 16); }
+
+// round-to-nearest-even, NaN stays NaN
+__device__ __forceinline__ uint32_t f32_to_bf16(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (u >> 16) | 0x40u;
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return u >> 16;
+}
+
+template <typename T, int V>
+struct Io;
+
+template <int V>
+struct Io<float, V> {
+  static __device__ __forceinline__ void load(const float* p, float (&x)[V]) {
+    if constexpr (V == 4) {
+      const float4 t = *reinterpret_cast<const float4*>(p);
+      x[0] = t.x; x[1] = t.y; x[2] = t.z; x[3] = t.w;
+    } else if constexpr (V == 2) {
+      const float2 t = *reinterpret_cast<const float2*>(p);
+      x[0] = t.x; x[1] = t.y;
+    } else {
+      x[0] = *p;
+    }
+  }
+  static __device__ __forceinline__ void store(float* p, const float (&x)[V]) {
+    if constexpr (V == 4) {
+      *reinterpret_cast<float4*>(p) = make_float4(x[0], x[1], x[2], x[3]);
+    } else if constexpr (V == 2) {
+      *reinterpret_cast<float2*>(p) = make_float2(x[0], x[1]);
+    } else {
+      *p = x[0];
+    }
+  }
+};
+
+template <int V>
+struct Io<uint16_t, V> {  // bf16 storage
+  static __device__ __forceinline__ void load(const uint16_t* p, float (&x)[V]) {
+    if constexpr (V == 8) {
+      const uint4 t = *reinterpret_cast<const uint4*>(p);
+      const uint32_t w[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        x[2 * i] = __uint_as_float(w[i] << 16);
+        x[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+      }
+    } else if constexpr (V == 4) {
+      const uint2 t = *reinterpret_cast<const uint2*>(p);
+      x[0] = __uint_as_float(t.x << 16); x[1] = __uint_as_float(t.x & 0xffff0000u);
+      x[2] = __uint_as_float(t.y << 16); x[3] = __uint_as_float(t.y & 0xffff0000u);
+    } else if constexpr (V == 2) {
+      const uint32_t t = *reinterpret_cast<const uint32_t*>(p);
+      x[0] = __uint_as_float(t << 16); x[1] = __uint_as_float(t & 0xffff0000u);
+    } else {
+      x[0] = bf16_to_f32(*p);
+    }
+  }
+  static __device__ __forceinline__ void store(uint16_t* p, const float (&x)[V]) {
+    if constexpr (V == 8) {
+      uint4 t;
+      t.x = f32_to_bf16(x[0]) | (f32_to_bf16(x[1]) << 16);
+      t.y = f32_to_bf16(x[2]) | (f32_to_bf16(x[3]) << 16);
+      t.z = f32_to_bf16(x[4]) | (f32_to_bf16(x[5]) << 16);
+      t.w = f32_to_bf16(x[6]) | (f32_to_bf16(x[7]) << 16);
+      *reinterpret_cast<uint4*>(p) = t;
+    } else if constexpr (V == 4) {
+      uint2 t;
+      t.x = f32_to_bf16(x[0]) | (f32_to_bf16(x[1]) << 16);
+      t.y = f32_to_bf16(x[2]) | (f32_to_bf16(x[3]) << 16);
+      *reinterpret_cast<uint2*>(p) = t;
+    } else if constexpr (V == 2) {
+      *reinterpret_cast<uint32_t*>(p) = f32_to_bf16(x[0]) | (f32_to_bf16(x[1]) << 16);
+    } else {
+      *p = (uint16_t)f32_to_bf16(x[0]);
+    }
+  }
+};
+
+}  // namespace appnp

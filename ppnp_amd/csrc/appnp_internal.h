@@ -1,0 +1,46 @@
+// appnp_internal.h -- host-side internals shared by the translation units of libppnp_amd.so.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "appnp_device.h"
+
+struct appnp_graph {
+  int64_t n = 0;         // global node count
+  int64_t row_lo = 0;    // held rows [row_lo, row_hi)
+  int64_t row_hi = 0;
+  int64_t nnz_hat = 0;   // nnz of the held A_hat rows
+  int64_t nnz_local = 0, nnz_remote = 0;
+  int mode = 0;          // APPNP_NORM_SYM / APPNP_NORM_RW
+  int symmetric = 0;     // A's pattern and weights are symmetric
+  int split = 0;         // local/remote CSRs present
+  int device = 0;
+  int32_t* row_ptr = nullptr;   // [rows+1]
+  int32_t* col = nullptr;       // [nnz_hat]
+  float* val = nullptr;         // [nnz_hat]
+  int32_t* lrow_ptr = nullptr;  // local-column CSR (split only)
+  int32_t* lcol = nullptr;
+  float* lval = nullptr;
+  int32_t* rrow_ptr = nullptr;  // remote-column CSR (split only)
+  int32_t* rcol = nullptr;
+  float* rval = nullptr;
+  double* dinv = nullptr;       // [n] 1/sqrt(D) (sym) or 1/D (rw), fp64
+};
+
+namespace appnp {
+
+// appnp_graph.hip
+int graph_build(const int32_t* indptr, const int32_t* indices, const float* vals, int64_t n,
+                int64_t nnz, int mode, int64_t row_lo, int64_t row_hi, int split,
+                hipStream_t s, appnp_graph* g);
+void graph_free(appnp_graph* g);
+
+// appnp_spmm.hip
+int pick_vec(int dtype, int64_t f, const int64_t* lds, int n_ld, const void* const* ptrs,
+             int n_ptr);
+hipError_t launch_step(int dtype, int epi, int V, const StepArgs& a, hipStream_t s);
+hipError_t launch_scale_rows(int dtype, const void* src, int64_t ld_src, void* dst,
+                             int64_t ld_dst, int64_t n, int64_t f, float alpha, hipStream_t s);
+
+}  // namespace appnp

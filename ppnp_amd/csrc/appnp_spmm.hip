@@ -1,0 +1,318 @@
+// appnp_spmm.hip -- one fused APPNP iteration as a CSR x dense SpMM + AXPBY kernel (gfx950).
+//
+//   Zout[i] = (1-alpha) * sum_j (M_k o A_hat)_ij * Zin[j]  +  alpha * H[i]
+//
+// Replaces the dense propagation product of the reference, model.py:63
+// (`self.ppr[idx] @ self.encoder(X)`), by its K-truncated Neumann series.
+//
+// The contraction is sparse, so the roofline is HBM (gather) bandwidth, not MFMA.  Layout:
+// a row of Z is F contiguous elements (row-major, leading dim ld); each lane owns V
+// consecutive features (16-byte vectors where F and ld allow) and a "group" of G lanes covers
+// one row slab of G*V features (blockIdx.y selects the slab when F > 64*V).
+//
+// Two kernel shapes:
+//   wide   (G >= 16): one wavefront per row.  The wave loads the row's (col, val) pairs 64 at
+//          a time with one coalesced load per lane, stages them in a per-wave LDS tile, and its
+//          P = 64/G sub-groups walk the tile interleaved (entry t goes to sub-group t % P),
+//          each lane gathering V features of Zin[col] per entry, U entries in flight.
+//          Sub-group partial sums are combined with a butterfly (fixed order, deterministic).
+//   narrow (G <= 8):  one G-lane group per row, P rows per wave (small F: 3/7/15 features).
+// Both fuse the dropout mask, the (1-alpha) scale and the alpha*H AXPBY into the epilogue, so
+// every iteration is a single launch that reads CSR + Zin gathers + H and writes Zout once.
+#include <algorithm>
+#include <cstdlib>
+
+#include "appnp_device.h"
+
+namespace appnp {
+
+namespace {
+
+template <typename T, int V, int EPI>
+__device__ __forceinline__ void epilogue(const StepArgs& a, int64_t row, int col0,
+                                         const float (&acc)[V], const float (&hv)[V]) {
+  float y[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) y[v] = a.scale * acc[v];
+  if constexpr (EPI == EPI_FWD) {
+#pragma unroll
+    for (int v = 0; v < V; ++v) y[v] = fmaf(a.alpha, hv[v], y[v]);
+    Io<T, V>::store(static_cast<T*>(a.out) + row * a.ld_out + col0, y);
+  } else if constexpr (EPI == EPI_BWD) {
+    if (a.out) Io<T, V>::store(static_cast<T*>(a.out) + row * a.ld_out + col0, y);
+    T* d = static_cast<T*>(a.aux) + row * a.ld_aux + col0;
+    float dv[V];
+    Io<T, V>::load(d, dv);
+#pragma unroll
+    for (int v = 0; v < V; ++v) dv[v] = fmaf(a.alpha, y[v], dv[v]);
+    Io<T, V>::store(d, dv);
+  } else if constexpr (EPI == EPI_PARTIAL) {
+    Io<float, V>::store(static_cast<float*>(a.out) + row * a.ld_out + col0, y);
+  } else {  // EPI_FINISH
+    float pv[V];
+    Io<float, V>::load(static_cast<const float*>(a.aux) + row * a.ld_aux + col0, pv);
+#pragma unroll
+    for (int v = 0; v < V; ++v) y[v] = fmaf(a.alpha, hv[v], y[v] + pv[v]);
+    Io<T, V>::store(static_cast<T*>(a.out) + row * a.ld_out + col0, y);
+  }
+}
+
+template <typename T, int V, int EPI>
+__device__ __forceinline__ void load_h(const StepArgs& a, int64_t row, int col0, float (&hv)[V]) {
+  if constexpr (EPI == EPI_FWD || EPI == EPI_FINISH) {
+    Io<T, V>::load(static_cast<const T*>(a.h) + row * a.ld_h + col0, hv);
+  } else {
+#pragma unroll
+    for (int v = 0; v < V; ++v) hv[v] = 0.0f;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// wide: one wavefront per row, P = 64/G sub-groups split the row's entries
+// ------------------------------------------------------------------------------------------
+template <typename T, int V, int G, int EPI, int U>
+__global__ __launch_bounds__(kBlock) void k_step_wide(StepArgs a) {
+  constexpr int P = kWave / G;
+  __shared__ int2 stage[kWavesPerBlock][kWave];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int sub = lane / G;
+  const int gl = lane % G;
+  const int col0 = blockIdx.y * (G * V) + gl * V;
+  const bool fact = col0 < a.f;
+  const T* __restrict__ zin = static_cast<const T*>(a.zin);
+  int2* tile = stage[wave];
+  const int64_t nwaves = (int64_t)gridDim.x * kWavesPerBlock;
+
+  for (int64_t row = (int64_t)blockIdx.x * kWavesPerBlock + wave; row < a.n_rows; row += nwaves) {
+    const int beg = a.row_ptr[row];
+    const int end = a.row_ptr[row + 1];
+    float hv[V];
+    if (sub == 0 && fact) load_h<T, V, EPI>(a, row, col0, hv);
+    float acc[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) acc[v] = 0.0f;
+
+    for (int cb = beg; cb < end; cb += kWave) {
+      const int n = min(kWave, end - cb);
+      int c = 0;
+      float w = 0.0f;
+      if (lane < n) {
+        c = a.col[cb + lane];
+        w = edge_weight(a.val[cb + lane], a.row_lo + row, c, a);
+      }
+      tile[lane] = make_int2(c, __float_as_int(w));
+      __builtin_amdgcn_wave_barrier();
+      for (int t = sub; t < n; t += P * U) {
+        int2 e[U];
+        float z[U][V];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int idx = t + u * P;
+          e[u] = idx < n ? tile[idx] : make_int2(0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (fact && t + u * P < n) {
+            Io<T, V>::load(zin + (int64_t)e[u].x * a.ld_in + col0, z[u]);
+          } else {
+#pragma unroll
+            for (int v = 0; v < V; ++v) z[u][v] = 0.0f;
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const float wu = __int_as_float(e[u].y);
+#pragma unroll
+          for (int v = 0; v < V; ++v) acc[v] = fmaf(wu, z[u][v], acc[v]);
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    // combine the P sub-group partial sums (butterfly, fixed order)
+#pragma unroll
+    for (int off = G; off < kWave; off <<= 1) {
+#pragma unroll
+      for (int v = 0; v < V; ++v) acc[v] += __shfl_xor(acc[v], off);
+    }
+    if (sub == 0 && fact) epilogue<T, V, EPI>(a, row, col0, acc, hv);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// narrow: one G-lane group per row, P = 64/G rows per wave
+// ------------------------------------------------------------------------------------------
+template <typename T, int V, int G, int EPI, int U>
+__global__ __launch_bounds__(kBlock) void k_step_narrow(StepArgs a) {
+  constexpr int P = kWave / G;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave = threadIdx.x >> 6;
+  const int sub = lane / G;
+  const int gl = lane % G;
+  const int col0 = blockIdx.y * (G * V) + gl * V;
+  const bool fact = col0 < a.f;
+  const T* __restrict__ zin = static_cast<const T*>(a.zin);
+  const int64_t stride = (int64_t)gridDim.x * kWavesPerBlock * P;
+
+  for (int64_t rb = ((int64_t)blockIdx.x * kWavesPerBlock + wave) * P; rb < a.n_rows;
+       rb += stride) {
+    const int64_t row = rb + sub;
+    if (row >= a.n_rows) continue;
+    const int beg = a.row_ptr[row];
+    const int end = a.row_ptr[row + 1];
+    float hv[V];
+    if (fact) load_h<T, V, EPI>(a, row, col0, hv);
+    float acc[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) acc[v] = 0.0f;
+    for (int e = beg; e < end; e += U) {
+      int c[U];
+      float w[U];
+      float z[U][V];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (e + u < end) {
+          c[u] = a.col[e + u];
+          w[u] = edge_weight(a.val[e + u], a.row_lo + row, c[u], a);
+        } else {
+          c[u] = 0;
+          w[u] = 0.0f;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (fact && e + u < end) {
+          Io<T, V>::load(zin + (int64_t)c[u] * a.ld_in + col0, z[u]);
+        } else {
+#pragma unroll
+          for (int v = 0; v < V; ++v) z[u][v] = 0.0f;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+#pragma unroll
+        for (int v = 0; v < V; ++v) acc[v] = fmaf(w[u], z[u][v], acc[v]);
+      }
+    }
+    if (fact) epilogue<T, V, EPI>(a, row, col0, acc, hv);
+  }
+}
+
+template <typename T, int V, int EPI>
+hipError_t launch_g(int G, dim3 grid, const StepArgs& a, hipStream_t s) {
+  constexpr int UW = 4;  // entries in flight per sub-group (wide)
+  constexpr int UN = 4;  // entries in flight per row (narrow)
+  const dim3 block(kBlock);
+  switch (G) {
+    case 1: hipLaunchKernelGGL((k_step_narrow<T, V, 1, EPI, UN>), grid, block, 0, s, a); break;
+    case 2: hipLaunchKernelGGL((k_step_narrow<T, V, 2, EPI, UN>), grid, block, 0, s, a); break;
+    case 4: hipLaunchKernelGGL((k_step_narrow<T, V, 4, EPI, UN>), grid, block, 0, s, a); break;
+    case 8: hipLaunchKernelGGL((k_step_narrow<T, V, 8, EPI, UN>), grid, block, 0, s, a); break;
+    case 16: hipLaunchKernelGGL((k_step_wide<T, V, 16, EPI, UW>), grid, block, 0, s, a); break;
+    case 32: hipLaunchKernelGGL((k_step_wide<T, V, 32, EPI, UW>), grid, block, 0, s, a); break;
+    case 64: hipLaunchKernelGGL((k_step_wide<T, V, 64, EPI, UW>), grid, block, 0, s, a); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+template <typename T, int EPI>
+hipError_t launch_v(int V, int G, dim3 grid, const StepArgs& a, hipStream_t s) {
+  switch (V) {
+    case 1: return launch_g<T, 1, EPI>(G, grid, a, s);
+    case 2: return launch_g<T, 2, EPI>(G, grid, a, s);
+    case 4: return launch_g<T, 4, EPI>(G, grid, a, s);
+    case 8:
+      if constexpr (sizeof(T) == 2) return launch_g<T, 8, EPI>(G, grid, a, s);
+      return hipErrorInvalidValue;
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace
+
+// Largest vector width (elements) valid for every operand: F, all leading dims and all
+// base pointers must be multiples of V elements.
+int pick_vec(int dtype, int64_t f, const int64_t* lds, int n_ld, const void* const* ptrs,
+             int n_ptr) {
+  const int es = dtype == 0 ? 4 : 2;
+  int v = dtype == 0 ? 4 : 8;
+  for (; v > 1; v >>= 1) {
+    bool ok = (f % v) == 0;
+    for (int i = 0; i < n_ld && ok; ++i) ok = (lds[i] % v) == 0;
+    for (int i = 0; i < n_ptr && ok; ++i)
+      ok = ptrs[i] == nullptr || (reinterpret_cast<uintptr_t>(ptrs[i]) % (uintptr_t)(v * es)) == 0;
+    if (ok) break;
+  }
+  return v;
+}
+
+static int env_int(const char* name, int dflt) {
+  const char* s = getenv(name);
+  return (s && *s) ? atoi(s) : dflt;
+}
+
+hipError_t launch_step(int dtype, int epi, int V, const StepArgs& a, hipStream_t s) {
+  if (a.n_rows <= 0 || a.f <= 0) return hipSuccess;
+  // lanes per row slab: smallest power of two covering min(F, 64V) features
+  const int64_t lanes_needed = (std::min<int64_t>(a.f, 64LL * V) + V - 1) / V;
+  int G = 1;
+  while (G < lanes_needed) G <<= 1;
+  const int64_t slabs = (a.f + (int64_t)G * V - 1) / ((int64_t)G * V);
+  const int64_t rows_per_block = G >= 16 ? kWavesPerBlock : (int64_t)kWavesPerBlock * (kWave / G);
+  static const int max_blocks = env_int("APPNP_MAX_BLOCKS", 256 * 8);
+  int64_t blocks = (a.n_rows + rows_per_block - 1) / rows_per_block;
+  if (blocks > max_blocks) blocks = max_blocks;
+  const dim3 grid((unsigned)blocks, (unsigned)slabs);
+  if (dtype == 0) {
+    switch (epi) {
+      case EPI_FWD: return launch_v<float, EPI_FWD>(V, G, grid, a, s);
+      case EPI_BWD: return launch_v<float, EPI_BWD>(V, G, grid, a, s);
+      case EPI_PARTIAL: return launch_v<float, EPI_PARTIAL>(V, G, grid, a, s);
+      case EPI_FINISH: return launch_v<float, EPI_FINISH>(V, G, grid, a, s);
+    }
+  } else {
+    switch (epi) {
+      case EPI_FWD: return launch_v<uint16_t, EPI_FWD>(V, G, grid, a, s);
+      case EPI_BWD: return launch_v<uint16_t, EPI_BWD>(V, G, grid, a, s);
+    }
+  }
+  return hipErrorInvalidValue;
+}
+
+// ------------------------------------------------------------------------------------------
+// small helpers: dst[i, :f] = alpha * src[i, :f]   (dH init of the adjoint; K = 0 copy)
+// ------------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_scale_rows(const T* __restrict__ src, int64_t ld_src,
+                                                       T* __restrict__ dst, int64_t ld_dst,
+                                                       int64_t n, int64_t f, float alpha) {
+  const int64_t total = n * f;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * kBlock) {
+    const int64_t r = i / f, c = i - r * f;
+    float x[1];
+    Io<T, 1>::load(src + r * ld_src + c, x);
+    x[0] *= alpha;
+    Io<T, 1>::store(dst + r * ld_dst + c, x);
+  }
+}
+
+hipError_t launch_scale_rows(int dtype, const void* src, int64_t ld_src, void* dst,
+                             int64_t ld_dst, int64_t n, int64_t f, float alpha, hipStream_t s) {
+  const int64_t total = n * f;
+  if (total <= 0) return hipSuccess;
+  int64_t blocks = (total + kBlock - 1) / kBlock;
+  if (blocks > 4096) blocks = 4096;
+  if (dtype == 0)
+    hipLaunchKernelGGL(k_scale_rows<float>, dim3((unsigned)blocks), dim3(kBlock), 0, s,
+                       static_cast<const float*>(src), ld_src, static_cast<float*>(dst), ld_dst,
+                       n, f, alpha);
+  else
+    hipLaunchKernelGGL(k_scale_rows<uint16_t>, dim3((unsigned)blocks), dim3(kBlock), 0, s,
+                       static_cast<const uint16_t*>(src), ld_src, static_cast<uint16_t*>(dst),
+                       ld_dst, n, f, alpha);
+  return hipGetLastError();
+}
+
+}  // namespace appnp

@@ -1,0 +1,132 @@
+"""Device-resident A_hat: the MI355X replacement for helpers.calc_A_hat / compute_ppr.
+
+Reference: /root/reference/helpers.py:58-66 (calc_A_hat) builds A_hat on the host in fp64
+scipy; helpers.py:68-71 (compute_ppr) then forms the dense N x N PPR matrix with an O(N^3)
+inverse.  Here the CSR of A is copied to the GPU once and ``appnp_graph_create`` builds
+A_hat there (fp64 arithmetic, fp32 storage, bit-identical to float32 of the reference).
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import torch
+
+from . import _lib
+
+
+def _stream_ptr(device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _ptr(t):
+    return C.c_void_p(t.data_ptr()) if t is not None and t.numel() > 0 else None
+
+
+class Graph:
+    """A_hat = calc_A_hat(adj, mode) held on one GPU (all rows, or rows [row_lo, row_hi)).
+
+    Build it with :meth:`from_scipy` (host CSR) or :meth:`from_csr` (torch CSR arrays).
+    """
+
+    def __init__(self, handle, device, keep_alive=()):
+        self._h = handle
+        self.device = torch.device(device)
+        self._keep = keep_alive
+        lib = _lib.load()
+        n, lo, hi, nnz = C.c_int64(), C.c_int64(), C.c_int64(), C.c_int64()
+        mode, sym = C.c_int(), C.c_int()
+        _lib.check(
+            "appnp_graph_info",
+            lib.appnp_graph_info(self._h, C.byref(n), C.byref(lo), C.byref(hi), C.byref(nnz),
+                                 C.byref(mode), C.byref(sym)),
+        )
+        self.n, self.row_lo, self.row_hi, self.nnz_hat = n.value, lo.value, hi.value, nnz.value
+        self.mode = {0: "sym", 1: "rw"}[mode.value]
+        self.symmetric = bool(sym.value)
+
+    # -- construction ---------------------------------------------------------------------
+    @classmethod
+    def from_csr(cls, indptr, indices, data, n, mode="sym", device=None, row_lo=0,
+                 row_hi=None, split_local=False):
+        """indptr/indices (int32) and optional data (fp32) of A; tensors or arrays."""
+        if mode not in _lib.NORM:
+            raise ValueError(f"mode must be 'sym' or 'rw', got {mode!r}")
+        device = torch.device(device if device is not None else "cuda")
+        if device.type != "cuda":
+            raise ValueError("ppnp_amd.Graph lives on a GPU (no CPU fallback)")
+        ip = torch.as_tensor(np.asarray(indptr) if not torch.is_tensor(indptr) else indptr)
+        ix = torch.as_tensor(np.asarray(indices) if not torch.is_tensor(indices) else indices)
+        ip = ip.to(device=device, dtype=torch.int32).contiguous()
+        ix = ix.to(device=device, dtype=torch.int32).contiguous()
+        dv = None
+        if data is not None:
+            d = torch.as_tensor(np.asarray(data) if not torch.is_tensor(data) else data)
+            dv = d.to(device=device, dtype=torch.float32).contiguous()
+            if bool((dv == 1).all()):
+                dv = None  # unweighted: the kernel substitutes 1.0
+        n = int(n)
+        if ip.numel() != n + 1:
+            raise ValueError("indptr must have n+1 entries")
+        nnz = int(ix.numel())
+        row_hi = n if row_hi is None else int(row_hi)
+        lib = _lib.load()
+        out = C.c_void_p()
+        with torch.cuda.device(device):
+            rc = lib.appnp_graph_create_rows(
+                _ptr(ip), _ptr(ix), _ptr(dv), n, nnz, _lib.NORM[mode], int(row_lo), row_hi,
+                1 if split_local else 0, C.c_void_p(_stream_ptr(device)), C.byref(out),
+            )
+        _lib.check("appnp_graph_create", rc)
+        return cls(out, device)
+
+    @classmethod
+    def from_scipy(cls, adj, mode="sym", device=None, **kw):
+        import scipy.sparse as sp
+
+        a = sp.csr_matrix(adj)
+        if not a.has_sorted_indices:
+            a = a.copy()
+            a.sort_indices()
+        return cls.from_csr(a.indptr.astype(np.int32), a.indices.astype(np.int32),
+                            a.data.astype(np.float32), a.shape[0], mode=mode, device=device, **kw)
+
+    # -- inspection -----------------------------------------------------------------------
+    @property
+    def handle(self):
+        return self._h
+
+    @property
+    def rows(self) -> int:
+        return self.row_hi - self.row_lo
+
+    def csr(self):
+        """(row_ptr int32, col int32, val fp32, dinv fp64) as new device tensors."""
+        lib = _lib.load()
+        rp = torch.empty(self.rows + 1, dtype=torch.int32, device=self.device)
+        col = torch.empty(self.nnz_hat, dtype=torch.int32, device=self.device)
+        val = torch.empty(self.nnz_hat, dtype=torch.float32, device=self.device)
+        dinv = torch.empty(self.n, dtype=torch.float64, device=self.device)
+        with torch.cuda.device(self.device):
+            rc = lib.appnp_graph_copy_csr(self._h, _ptr(rp), _ptr(col), _ptr(val), _ptr(dinv),
+                                          C.c_void_p(_stream_ptr(self.device)))
+        _lib.check("appnp_graph_copy_csr", rc)
+        return rp, col, val, dinv
+
+    def close(self):
+        if getattr(self, "_h", None) is not None:
+            try:
+                _lib.load().appnp_graph_destroy(self._h)
+            finally:
+                self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __repr__(self):
+        return (f"Graph(n={self.n}, rows=[{self.row_lo},{self.row_hi}), nnz_hat={self.nnz_hat}, "
+                f"mode={self.mode!r}, symmetric={self.symmetric}, device={self.device})")

@@ -1,0 +1,143 @@
+"""Model surface: the reference's PPNP plus the APPNP drop-in on the HIP propagation path.
+
+Mirrors /root/reference/model.py:
+  CustomLinear  model.py:13-38   (weight laid out (in, out), fan_out Kaiming init, addmm)
+  PPNP          model.py:41-67   (dense precomputed PPR; kept unchanged for callers that pass
+                                  ``ppr=``, e.g. batch-main.py:140-146)
+  APPNP         new              same constructor/forward/get_norm surface as PPNP, but the
+                                  propagation ``ppr[idx] @ H`` (model.py:63) is computed as
+                                  Z_K[idx] by K fused HIP SpMM launches over A_hat built on
+                                  the GPU (helpers.py:58-66) -- no N x N matrix exists.
+"""
+
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+from torch import nn
+
+from .graph import Graph
+from .ops import propagate
+
+
+class CustomLinear(nn.Module):
+    """model.py:13-38."""
+
+    def __init__(self, in_features, out_features, bias=True):
+        super().__init__()
+        self.in_features = in_features
+        self.out_features = out_features
+        self.weight = nn.Parameter(torch.Tensor(in_features, out_features))
+        if bias:
+            self.bias = nn.Parameter(torch.Tensor(out_features))
+        else:
+            self.register_parameter("bias", None)
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        nn.init.kaiming_uniform_(self.weight, mode="fan_out", a=math.sqrt(5))
+        if self.bias is not None:
+            _, fan_out = nn.init._calculate_fan_in_and_fan_out(self.weight)
+            bound = 1 / math.sqrt(fan_out)
+            nn.init.uniform_(self.bias, -bound, bound)
+
+    def forward(self, input):
+        if self.bias is None:
+            return input @ self.weight
+        return torch.addmm(self.bias, input, self.weight)
+
+
+def _encoder(n_features, n_classes, hidden_dim, drop_prob, bias):
+    # model.py:46-52
+    return nn.Sequential(
+        nn.Dropout(drop_prob),
+        CustomLinear(n_features, hidden_dim, bias=bias),
+        nn.ReLU(inplace=True),
+        nn.Dropout(drop_prob),
+        nn.Linear(hidden_dim, n_classes, bias=bias),
+    )
+
+
+class PPNP(nn.Module):
+    """model.py:41-67, unchanged semantics (dense ``ppr`` buffer)."""
+
+    def __init__(self, n_features, n_classes, ppr, hidden_dim=64, drop_prob=0.5, bias=False):
+        super().__init__()
+        self.encoder = _encoder(n_features, n_classes, hidden_dim, drop_prob, bias)
+        self.register_buffer("ppr", ppr)
+        self._reg_params = list(self.encoder[1].parameters())
+
+    def get_norm(self):
+        return sum((torch.sum(param ** 2) for param in self._reg_params))
+
+    def forward(self, X, idx=None, ppr=None):
+        if idx is not None:
+            return self.ppr[idx] @ self.encoder(X)
+        elif ppr is not None:
+            return ppr @ self.encoder(X)
+        else:
+            raise Exception()
+
+
+class APPNP(nn.Module):
+    """Drop-in for PPNP on the gfx950 propagation path.
+
+    ``adj`` is the (standardized) adjacency as a scipy sparse matrix, exactly what the
+    reference passes to ``compute_ppr`` (main.py:106).  It is stored as CSR buffers so
+    ``.cuda()`` / ``.to()`` move it like the reference's ``ppr`` buffer; A_hat is built on
+    the device at the first forward on that device.
+
+    forward(X, idx)      -> Z_K[idx]          (model.py:63 semantics, PPR truncated at K)
+    forward(X, ppr=P)    -> P @ encoder(X)    (model.py:65, batch mode, dense P unchanged)
+    forward(X)           -> raises Exception() (model.py:66-67)
+
+    ``edge_drop`` > 0 applies edge dropout inside the propagation kernel in training mode.
+    """
+
+    def __init__(self, n_features, n_classes, adj, alpha=0.1, K=10, hidden_dim=64,
+                 drop_prob=0.5, bias=False, mode="sym", edge_drop=0.0, dtype=torch.float32):
+        super().__init__()
+        import scipy.sparse as sp
+
+        self.encoder = _encoder(n_features, n_classes, hidden_dim, drop_prob, bias)
+        self._reg_params = list(self.encoder[1].parameters())
+        a = sp.csr_matrix(adj)
+        if not a.has_sorted_indices:
+            a = a.copy()
+            a.sort_indices()
+        self.n_nodes = int(a.shape[0])
+        self.register_buffer("adj_indptr", torch.from_numpy(a.indptr.astype(np.int32)))
+        self.register_buffer("adj_indices", torch.from_numpy(a.indices.astype(np.int32)))
+        self.register_buffer("adj_data", torch.from_numpy(a.data.astype(np.float32)))
+        self.alpha = float(alpha)
+        self.K = int(K)
+        self.mode = mode
+        self.edge_drop = float(edge_drop)
+        self.prop_dtype = dtype
+        self._graph = None
+
+    def graph(self) -> Graph:
+        dev = self.adj_indptr.device
+        if self._graph is None or self._graph.device != dev:
+            self._graph = Graph.from_csr(self.adj_indptr, self.adj_indices, self.adj_data,
+                                         self.n_nodes, mode=self.mode, device=dev)
+        return self._graph
+
+    def get_norm(self):
+        return sum((torch.sum(param ** 2) for param in self._reg_params))
+
+    def propagate(self, H):
+        p = self.edge_drop if self.training else 0.0
+        seed = int(torch.randint(0, 2**62, (1,)).item()) if p > 0 else 0
+        Hc = H.to(self.prop_dtype)
+        return propagate(self.graph(), Hc, self.K, self.alpha, p, seed).to(H.dtype)
+
+    def forward(self, X, idx=None, ppr=None):
+        if idx is not None:
+            return self.propagate(self.encoder(X))[idx]
+        elif ppr is not None:
+            return ppr @ self.encoder(X)
+        else:
+            raise Exception()

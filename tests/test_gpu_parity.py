@@ -1,0 +1,308 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle and the reference fixtures.
+
+Tolerances (north_star: "within a stated fp32 tolerance"):
+  fp32 storage : max|Z - Z_ref| <= 1e-5 * max|Z_ref| + 1e-6   
+  bf16 storage : max|Z - Z_ref| <= 2e-2 * max|Z_ref|, argmax agreement >= 0.98 (section 7 step 5)
+  A_hat build  : bit-exact (int32 structure, fp32 values == float32(reference fp64))
+"""
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+import torch
+
+from oracle import ppnp_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+def _lib():
+    import ppnp_amd
+
+    return ppnp_amd
+
+
+def adj_of(g, prefix="adj"):
+    n = int(g["n"])
+    return sp.csr_matrix((g[f"{prefix}_data"], g[f"{prefix}_indices"], g[f"{prefix}_indptr"]),
+                         shape=(n, n))
+
+
+def close_fp32(Z, ref):
+    Z = np.asarray(Z, dtype=np.float64)
+    err = np.abs(Z - ref).max()
+    tol = 1e-5 * np.abs(ref).max() + 1e-6
+    assert err <= tol, f"max err {err:.3e} > tol {tol:.3e}"
+
+
+def to_np(t):
+    return t.float().cpu().numpy().astype(np.float64)
+
+
+# ---------------------------------------------------------------------------------------
+# A_hat construction (helpers.py:58-66) -- bit-exact
+# ---------------------------------------------------------------------------------------
+
+
+@pytest.mark.parametrize("ds", ["cora", "citeseer"])
+@pytest.mark.parametrize("mode", ["sym", "rw"])
+def test_graph_build_bit_exact(ds, mode, request):
+    g = request.getfixturevalue(ds)
+    pa = _lib()
+    G = pa.Graph.from_scipy(adj_of(g), mode=mode, device=DEV)
+    rp, col, val, _ = G.csr()
+    assert np.array_equal(rp.cpu().numpy(), g[f"ahat_{mode}_indptr"])
+    assert np.array_equal(col.cpu().numpy(), g[f"ahat_{mode}_indices"])
+    ref = g[f"ahat_{mode}_data"].astype(np.float32)
+    assert np.array_equal(val.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+    assert G.symmetric
+
+
+@pytest.mark.parametrize("name", ["complete5", "complete2", "path3", "isolated3", "weighted4",
+                                  "selfloop3"])
+@pytest.mark.parametrize("mode", ["sym", "rw"])
+def test_graph_build_kat(kat, name, mode):
+    pa = _lib()
+    n = len(kat[f"{name}_indptr"]) - 1
+    G = pa.Graph.from_csr(kat[f"{name}_indptr"], kat[f"{name}_indices"], kat[f"{name}_data"], n,
+                          mode=mode, device=DEV)
+    rp, col, val, _ = G.csr()
+    dense = sp.csr_matrix((val.cpu().numpy(), col.cpu().numpy(), rp.cpu().numpy()),
+                          shape=(n, n)).toarray()
+    ref = kat[f"{name}_ahat_{mode}_dense"].astype(np.float32)
+    assert np.array_equal(dense.astype(np.float32), ref)
+
+
+def test_graph_rejects_unsorted():
+    pa = _lib()
+    indptr = np.array([0, 2, 3, 4], dtype=np.int32)
+    indices = np.array([2, 1, 0, 0], dtype=np.int32)  # row 0 unsorted
+    with pytest.raises(pa._lib.AppnpError) as e:
+        pa.Graph.from_csr(indptr, indices, None, 3, device=DEV)
+    assert e.value.code == pa._lib.APPNP_EINVAL
+
+
+# ---------------------------------------------------------------------------------------
+# propagation vs the reference fixtures
+# ---------------------------------------------------------------------------------------
+
+
+@pytest.mark.parametrize("ds", ["cora", "citeseer"])
+@pytest.mark.parametrize("mode,K,alpha,key", [("sym", 10, 0.1, "Z_sym_K10_a0.1"),
+                                              ("sym", 20, 0.2, "Z_sym_K20_a0.2"),
+                                              ("rw", 10, 0.1, "Z_rw_K10_a0.1")])
+def test_propagate_fixture(ds, mode, K, alpha, key, request):
+    g = request.getfixturevalue(ds)
+    pa = _lib()
+    G = pa.Graph.from_scipy(adj_of(g), mode=mode, device=DEV)
+    H = torch.from_numpy(g["H"]).to(DEV)
+    Z = pa.propagate_forward(G, H, K, alpha)
+    close_fp32(to_np(Z), g[key])
+
+
+def test_propagate_converges_to_ppr(cora):
+    """K -> infinity limit equals compute_ppr(adj, a) @ H (helpers.py:68-71)."""
+    pa = _lib()
+    G = pa.Graph.from_scipy(adj_of(cora), device=DEV)
+    H = torch.from_numpy(cora["H"]).to(DEV)
+    Z = to_np(pa.propagate_forward(G, H, 200, 0.1))
+    ref = cora["pprH_a0.1"]
+    assert np.abs(Z - ref).max() <= 1e-5 * np.abs(ref).max()
+
+
+# ---------------------------------------------------------------------------------------
+# shapes, widths, dtypes, edge cases vs the oracle on seeded synthetic graphs
+# ---------------------------------------------------------------------------------------
+
+
+def synth(n, m, seed):
+    return O.synth_graph(n, m, seed)
+
+
+@pytest.mark.parametrize("F", [1, 2, 3, 4, 6, 7, 8, 15, 16, 33, 64, 100, 128, 256, 300, 520])
+def test_propagate_widths(F):
+    pa = _lib()
+    adj = synth(3000, 15000, seed=F)
+    G = pa.Graph.from_scipy(adj, device=DEV)
+    ah = O.calc_a_hat(adj, "sym")
+    H = torch.randn(3000, F, generator=torch.Generator().manual_seed(F))
+    Z = pa.propagate_forward(G, H.to(DEV), 10, 0.1)
+    close_fp32(to_np(Z), O.appnp_propagate(ah, H.numpy(), 10, 0.1))
+
+
+@pytest.mark.parametrize("K", [0, 1, 2, 3])
+def test_propagate_small_K(K):
+    pa = _lib()
+    adj = synth(500, 2000, seed=7)
+    G = pa.Graph.from_scipy(adj, device=DEV)
+    H = torch.randn(500, 12, generator=torch.Generator().manual_seed(1))
+    Z = pa.propagate_forward(G, H.to(DEV), K, 0.15)
+    close_fp32(to_np(Z), O.appnp_propagate(O.calc_a_hat(adj, "sym"), H.numpy(), K, 0.15))
+
+
+def test_propagate_padded_ld():
+    """H/Z with a leading dimension > F (row slices of a wider buffer)."""
+    pa = _lib()
+    adj = synth(800, 4000, seed=3)
+    G = pa.Graph.from_scipy(adj, device=DEV)
+    base = torch.randn(800, 40, generator=torch.Generator().manual_seed(2)).to(DEV)
+    H = base[:, :30]
+    Zbuf = torch.zeros(800, 36, device=DEV)
+    pa.propagate_forward(G, H, 5, 0.1, out=Zbuf[:, :30])
+    ref = O.appnp_propagate(O.calc_a_hat(adj, "sym"), H.cpu().numpy(), 5, 0.1)
+    close_fp32(to_np(Zbuf[:, :30]), ref)
+    assert torch.all(Zbuf[:, 30:] == 0)
+
+
+def test_propagate_isolated_and_weighted(kat):
+    pa = _lib()
+    for name in ("isolated3", "weighted4", "selfloop3"):
+        n = len(kat[f"{name}_indptr"]) - 1
+        for mode in ("sym", "rw"):
+            G = pa.Graph.from_csr(kat[f"{name}_indptr"], kat[f"{name}_indices"],
+                                  kat[f"{name}_data"], n, mode=mode, device=DEV)
+            H = torch.randn(n, 5, generator=torch.Generator().manual_seed(0))
+            Z = to_np(pa.propagate_forward(G, H.to(DEV), 300, 0.1))
+            ref = kat[f"{name}_ppr_{mode}_a0.1"] @ H.numpy().astype(np.float64)
+            assert np.abs(Z - ref).max() <= 1e-5 * np.abs(ref).max() + 1e-6
+
+
+def test_complete_graph_closed_form(kat):
+    """K_n: Z_K = a H + (1-a) mean_rows(H) for every K >= 1."""
+    pa = _lib()
+    n = 5
+    G = pa.Graph.from_csr(kat["complete5_indptr"], kat["complete5_indices"],
+                          kat["complete5_data"], n, device=DEV)
+    H = torch.randn(n, 9, generator=torch.Generator().manual_seed(5)).double()
+    ref = 0.1 * H + 0.9 * H.mean(0, keepdim=True)
+    for K in (1, 4, 10):
+        Z = to_np(pa.propagate_forward(G, H.float().to(DEV), K, 0.1))
+        assert np.abs(Z - ref.numpy()).max() < 1e-6
+
+
+def test_empty_and_edgeless():
+    pa = _lib()
+    # graph with nodes but no edges: A_hat = I -> Z = H
+    indptr = np.zeros(6, dtype=np.int32)
+    G = pa.Graph.from_csr(indptr, np.zeros(0, dtype=np.int32), None, 5, device=DEV)
+    H = torch.randn(5, 3).to(DEV)
+    assert torch.allclose(pa.propagate_forward(G, H, 10, 0.1), H, atol=1e-6)
+    # zero feature columns
+    Z = pa.propagate_forward(G, torch.zeros(5, 0, device=DEV), 10, 0.1)
+    assert Z.shape == (5, 0)
+
+
+def test_bf16_storage():
+    pa = _lib()
+    adj = synth(18333, 81894, seed=3)  # MS-Academic-sized (config 3)
+    G = pa.Graph.from_scipy(adj, device=DEV)
+    H = torch.randn(18333, 15, generator=torch.Generator().manual_seed(0))
+    Zb = to_np(pa.propagate_forward(G, H.bfloat16().to(DEV), 20, 0.2))
+    ref = O.appnp_propagate(O.calc_a_hat(adj, "sym"), H.bfloat16().float().numpy(), 20, 0.2)
+    assert np.abs(Zb - ref).max() <= 2e-2 * np.abs(ref).max()
+    assert (Zb.argmax(1) == ref.argmax(1)).mean() >= 0.98
+
+
+def test_deterministic():
+    pa = _lib()
+    adj = synth(5000, 40000, seed=11)
+    G = pa.Graph.from_scipy(adj, device=DEV)
+    H = torch.randn(5000, 100, generator=torch.Generator().manual_seed(3)).to(DEV)
+    a = pa.propagate_forward(G, H, 10, 0.1)
+    b = pa.propagate_forward(G, H, 10, 0.1)
+    assert torch.equal(a, b)
+
+
+# ---------------------------------------------------------------------------------------
+# edge dropout (bit-exact mask vs the oracle's counter hash) and backward
+# ---------------------------------------------------------------------------------------
+
+
+@pytest.mark.parametrize("p", [0.1, 0.5])
+def test_edge_dropout_matches_oracle(p):
+    pa = _lib()
+    adj = synth(2000, 10000, seed=5)
+    G = pa.Graph.from_scipy(adj, device=DEV)
+    H = torch.randn(2000, 16, generator=torch.Generator().manual_seed(9))
+    Z = to_np(pa.propagate_forward(G, H.to(DEV), 6, 0.1, p_drop=p, seed=1234))
+    ref = O.appnp_propagate(O.calc_a_hat(adj, "sym"), H.numpy(), 6, 0.1, p_drop=p, seed=1234)
+    close_fp32(Z, ref)
+    Z2 = to_np(pa.propagate_forward(G, H.to(DEV), 6, 0.1, p_drop=p, seed=1235))
+    assert np.abs(Z2 - Z).max() > 1e-3  # a different seed gives a different mask
+
+
+@pytest.mark.parametrize("p", [0.0, 0.3])
+@pytest.mark.parametrize("K", [1, 2, 5])
+def test_backward_matches_oracle(p, K):
+    pa = _lib()
+    adj = synth(1500, 6000, seed=2)
+    G = pa.Graph.from_scipy(adj, device=DEV)
+    dZ = torch.randn(1500, 8, generator=torch.Generator().manual_seed(4))
+    dH = to_np(pa.propagate_backward(G, dZ.to(DEV), K, 0.1, p_drop=p, seed=77))
+    ref = O.appnp_backward(O.calc_a_hat(adj, "sym"), dZ.numpy(), K, 0.1, p_drop=p, seed=77)
+    close_fp32(dH, ref)
+
+
+def test_autograd_gradcheck_small():
+    pa = _lib()
+    adj = synth(60, 200, seed=1)
+    G = pa.Graph.from_scipy(adj, device=DEV)
+    H = torch.randn(60, 4, device=DEV, requires_grad=True)
+    Z = pa.propagate(G, H, 4, 0.2, p_drop=0.2, seed=3)
+    W = torch.randn_like(Z)
+    (Z * W).sum().backward()
+    # <J H, W> == <H, J^T W> on the same mask (linearity in H)
+    Hd = H.detach()
+    lhs = (pa.propagate_forward(G, Hd, 4, 0.2, 0.2, 3) * W).sum().item()
+    rhs = (Hd * H.grad).sum().item()
+    assert abs(lhs - rhs) <= 1e-4 * max(1.0, abs(lhs))
+
+
+def test_backward_unsupported_for_rw():
+    pa = _lib()
+    adj = synth(100, 300, seed=1)
+    G = pa.Graph.from_scipy(adj, mode="rw", device=DEV)
+    with pytest.raises(pa._lib.AppnpError) as e:
+        pa.propagate_backward(G, torch.randn(100, 3, device=DEV), 3, 0.1)
+    assert e.value.code == pa._lib.APPNP_ENOTSUP
+
+
+# ---------------------------------------------------------------------------------------
+# model surface (model.py:41-67)
+# ---------------------------------------------------------------------------------------
+
+
+@pytest.mark.parametrize("ds", ["cora", "citeseer"])
+def test_ppnp_and_appnp_logits(ds, request):
+    g = request.getfixturevalue(ds)
+    pa = _lib()
+    n, C = int(g["n"]), int(g["n_classes"])
+    X = torch.from_numpy(g["ppnp_X"])
+    idx = torch.from_numpy(g["ppnp_idx"])
+    ref = g["ppnp_logits"]
+    # unchanged PPNP surface with the reference's dense ppr
+    ppr = torch.from_numpy(O.compute_ppr(adj_of(g), 0.1)).float()
+    net = pa.PPNP(n_features=X.shape[1], n_classes=C, ppr=ppr)
+    net.encoder[1].weight.data.copy_(torch.from_numpy(g["ppnp_W1"]))
+    net.encoder[4].weight.data.copy_(torch.from_numpy(g["ppnp_W2"]))
+    net = net.to(DEV).eval()
+    with torch.no_grad():
+        out = net(X.to(DEV), idx.to(DEV)).cpu().numpy()
+    assert np.abs(out - ref).max() <= 1e-4 * np.abs(ref).max()
+    # APPNP drop-in: same weights, HIP propagation with large K converges to the PPNP logits
+    ap = pa.APPNP(n_features=X.shape[1], n_classes=C, adj=adj_of(g), alpha=0.1, K=200)
+    ap.encoder.load_state_dict(net.encoder.state_dict())
+    ap = ap.to(DEV).eval()
+    with torch.no_grad():
+        out2 = ap(X.to(DEV), idx.to(DEV)).cpu().numpy()
+    assert np.abs(out2 - ref).max() <= 1e-4 * np.abs(ref).max()
+    with pytest.raises(Exception):
+        ap(X.to(DEV))
+    # batch mode (model.py:65)
+    sub = ppr[idx[:16]].to(DEV)
+    with torch.no_grad():
+        out3 = ap(X.to(DEV), idx=None, ppr=sub).cpu().numpy()
+    ref3 = g["ppnp_logits_ppr_mode"]
+    assert np.abs(out3 - ref3).max() <= 1e-4 * np.abs(ref3).max()
