@@ -1,0 +1,80 @@
+"""CPU: the C-ABI library loads and exports every symbol include/ppnp_amd.h declares.
+
+No compute call is made (there is no GPU here); only argument validation that returns
+before touching the device.
+"""
+
+import ctypes as C
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "ppnp_amd.h")
+
+
+def declared():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(appnp_[a-z_]+)\s*\(", src)))
+
+
+def test_header_declares_expected_entry_points():
+    names = declared()
+    for must in ("appnp_graph_create", "appnp_propagate", "appnp_propagate_bwd",
+                 "appnp_step", "appnp_workspace_bytes", "appnp_graph_destroy",
+                 "appnp_strerror"):
+        assert must in names
+
+
+def test_library_exports_all_declared_symbols():
+    from ppnp_amd import _lib
+
+    lib = _lib.load()
+    for name in declared():
+        assert hasattr(lib, name), f"missing export {name}"
+    assert set(_lib.EXPORTED) == set(declared())
+
+
+def test_abi_version_and_strerror():
+    from ppnp_amd import _lib
+
+    lib = _lib.load()
+    assert lib.appnp_abi_version() == 1
+    assert lib.appnp_strerror(0) == b"ok"
+    assert lib.appnp_strerror(_lib.APPNP_EINVAL) == b"invalid argument"
+    assert lib.appnp_strerror(_lib.APPNP_ENOTSUP) == b"not supported"
+
+
+def test_argument_validation_without_device():
+    """Errors are returned as codes, never raised/aborted across the ABI."""
+    from ppnp_amd import _lib
+
+    lib = _lib.load()
+    out = C.c_void_p()
+    # bad mode
+    assert lib.appnp_graph_create(None, None, None, 0, 0, 7, None, C.byref(out)) == _lib.APPNP_EINVAL
+    # negative sizes
+    assert lib.appnp_graph_create(None, None, None, -1, 0, 0, None, C.byref(out)) == _lib.APPNP_EINVAL
+    # n > int32 range
+    assert lib.appnp_graph_create(None, None, None, 2**31, 0, 0, None, C.byref(out)) == _lib.APPNP_ERANGE
+    # null graph handle
+    assert lib.appnp_propagate(None, None, 0, None, 0, 1, 0, 1, 0.1, 0.0, 0, None, 0, None) == _lib.APPNP_EINVAL
+    assert lib.appnp_propagate_bwd(None, None, 0, None, 0, 1, 0, 1, 0.1, 0.0, 0, None, 0, None) == _lib.APPNP_EINVAL
+    assert lib.appnp_step(None, 0, None, 0, None, 0, None, 0, None, 0, 1, 0, 0, 0.1, 0.0, 0, None) == _lib.APPNP_EINVAL
+    assert lib.appnp_workspace_bytes(None, 10, 10, 0) == 0
+    lib.appnp_graph_destroy(None)  # no-op
+
+
+def test_no_cpu_fallback_when_library_missing(tmp_path, monkeypatch):
+    """The product path fails loudly when the HIP extension is absent."""
+    import importlib
+
+    from ppnp_amd import _lib
+
+    monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "missing.so"))
+    monkeypatch.setattr(_lib, "_lib", None)
+    with pytest.raises(ImportError):
+        _lib.load()
+    importlib.reload(_lib)
