@@ -44,7 +44,13 @@ def parse():
     p.add_argument("--workload", default="products-synth")
     p.add_argument("--cpu-iters", type=int, default=2,
                    help="iterations of the CPU baseline sample (0 disables it)")
-    p.add_argument("--dist-mode", default="row", choices=["row", "row-overlap"])
+    p.add_argument("--layout", default="auto",
+                   help="multi-GPU layout: auto | row | col | RxC (row groups x column groups)")
+    p.add_argument("--emulate", default=None, metavar="P:r",
+                   help="single-GPU emulation of rank r of a P-rank --layout (kernel time of "
+                        "that rank only, no exchange; NOT a multi-GPU result)")
+    p.add_argument("--overlap", action="store_true",
+                   help="row layouts: overlap the all-gather with the local-column product")
     return p.parse_args()
 
 
@@ -82,28 +88,58 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # one GPU per rank; on a box with fewer GPUs than ranks (multi-process rehearsal) ranks
+    # share devices round-robin
+    ndev = max(1, torch.cuda.device_count())
+    dev = torch.device("cuda", local_rank % ndev)
+    torch.cuda.set_device(dev)
 
     import ppnp_amd
     from ppnp_amd import synth
+    from ppnp_amd import dist as pdist
 
     n, m, F, K, alpha, dtype = synth.CONFIGS[args.workload]
     seed = synth.SEEDS.get(args.workload, 0)
+    distributed = world > 1 or args.layout != "auto"
+    emu = {}
+    lw = world
+    if args.emulate:
+        P, r = (int(x) for x in args.emulate.split(":"))
+        emu = dict(rank=r, world=P, comm=pdist.NullComm())
+        lw = P
+    layout = (pdist.choose_layout(lw, n, F, m) if args.layout == "auto"
+              else pdist.Layout.parse(args.layout, lw))
+    if world > 1:
+        # RCCL only where the layout has a data-path exchange (row groups); a pure column
+        # layout has none, so its control plane (barrier, max-over-ranks) runs over gloo
+        backend = os.environ.get("PPNP_DIST_BACKEND") or ("nccl" if layout.rows > 1 else "gloo")
+        if backend == "nccl":
+            torch.distributed.init_process_group("nccl", device_id=dev)
+        else:
+            torch.distributed.init_process_group(backend)
+    ctl_dev = dev if world > 1 and torch.distributed.get_backend() == "nccl" else "cpu"
+
     t0 = time.perf_counter()
     indptr, indices = synth.uniform_graph_device(n, m, seed, device=dev)
     H = synth.features(n, F, dtype=dtype, device=dev)
     torch.cuda.synchronize()
     t_gen = time.perf_counter() - t0
 
-    if world > 1:
-        from ppnp_amd import dist as pdist
-
-        runner = pdist.RowPartitionAPPNP.create(indptr, indices, n, H, K, alpha, dev,
-                                                overlap=args.dist_mode == "row-overlap")
+    if distributed:
+        t1 = time.perf_counter()
+        runner = pdist.PartitionedAPPNP.create(indptr, indices, n, H, K, alpha, dev,
+                                               layout=layout, overlap=args.overlap, **emu)
+        torch.cuda.synchronize()
+        t_build = time.perf_counter() - t1
         graph = runner.graph
         run = runner.run
         stream = torch.cuda.current_stream(dev)
+        F_local = runner.width
+        mine = graph.nnz_hat if runner.layout.coords(runner.rank)[1] == 0 else 0
+        nnz_t = torch.tensor([mine], dtype=torch.int64, device=ctl_dev)
+        if world > 1:
+            torch.distributed.all_reduce(nnz_t)
+        nnz_total = int(nnz_t.item())
     else:
         t1 = time.perf_counter()
         graph = ppnp_amd.Graph.from_csr(indptr, indices, None, n, mode="sym", device=dev)
@@ -115,11 +151,13 @@ def main():
             ppnp_amd.propagate_forward(graph, H, K, alpha, out=Z)
 
         stream = torch.cuda.current_stream(dev)
+        F_local = F
+        nnz_total = graph.nnz_hat
     del indices
-    nnz_hat = graph.nnz_hat if world == 1 else runner.nnz_hat_total
     if rank == 0:
-        log(f"[bench] {args.workload}: N={n} nnz_hat={nnz_hat} F={F} K={K} dtype={dtype} "
-            f"gen {t_gen:.2f}s" + (f" build {t_build:.3f}s" if world == 1 else ""))
+        log(f"[bench] {args.workload}: N={n} nnz_hat={nnz_total} F={F} K={K} dtype={dtype} "
+            f"gen {t_gen:.2f}s build {t_build:.3f}s"
+            + (f" layout {runner.layout}" if distributed else ""))
 
     for _ in range(args.warmup):
         run()
@@ -141,7 +179,7 @@ def main():
     wall = time.perf_counter() - t0
     dev_ms = ev0.elapsed_time(ev1)
     if world > 1:
-        t = torch.tensor([wall, dev_ms], dtype=torch.float64, device=dev)
+        t = torch.tensor([wall, dev_ms], dtype=torch.float64, device=ctl_dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         wall, dev_ms = float(t[0]), float(t[1])
 
@@ -149,7 +187,7 @@ def main():
     rows_local = graph.rows
     nnz_local = graph.nnz_hat
     # dominant kernel: one SpMM launch per iteration per rank
-    b_iter = 4 * (rows_local + 1) + 8 * nnz_local + 3 * rows_local * F * s
+    b_iter = 4 * (rows_local + 1) + 8 * nnz_local + 3 * rows_local * F_local * s
     avg_launch_ms = dev_ms / (args.steps * K)
     achieved = b_iter / (avg_launch_ms * 1e-3) / 1e9
     value = n * F * K * args.steps / wall
@@ -170,12 +208,15 @@ def main():
         "config": {
             "workload": args.workload,
             "nodes": n,
-            "nnz_a_hat": nnz_hat,
+            "nnz_a_hat": nnz_total,
             "F": F,
             "K": K,
             "alpha": alpha,
             "norm": "sym",
-            "parallelism": f"row{world}" if world > 1 else "single",
+            "parallelism": (f"rows{runner.layout.rows}xcols{runner.layout.cols}"
+                            + ("-overlap" if args.overlap else "")
+                            + (f"-EMULATED-rank{args.emulate}" if args.emulate else ""))
+                           if distributed else "single",
         },
         "roofline": {
             "bound": "hbm",

@@ -1,0 +1,260 @@
+"""Multi-GPU APPNP propagation: one process per GPU, torch.distributed over RCCL (xGMI).
+
+SURVEY.md section 8(e).  P ranks are laid out as R row groups x C column (feature) groups:
+
+* row partition (the north_star design, R = P): rank r owns the A_hat rows and the H / Z rows
+  of [lo_r, hi_r).  Every iteration needs all of Z_k, so the ranks of one column group
+  all-gather their row shards of Z_{k+1} (RCCL all_gather_into_tensor, in place) -- the
+  path's one real exchange step.  With ``overlap=True`` each rank's rows are stored as a
+  local-column and a remote-column CSR (appnp_graph_create_rows split_local): the local
+  product of the next iteration runs while the all-gather is in flight, the remote product
+  after it lands (appnp_step PART_LOCAL / PART_REMOTE).
+* column partition (C = P): propagation is column-separable, so rank r takes a slab of
+  F/C features of H and Z and a full replica of A_hat; the K loop has no communication.
+  Each slab is stored with a line-friendly leading dimension (a 25-float slab in one 128-B
+  line), which is what makes this layout pay on MI355X: a random row gather costs cache-line
+  requests, and the chip serves ~55 G random line requests/s (profiles/r1_gather_probe.txt).
+* R x C mixes the two (e.g. 2 x 4 on 8 GPUs).
+
+The edge-dropout mask is keyed on (seed, k, global row, global col), so it does not depend on
+the layout.  The communication and per-step kernels are injectable (``comm``, ``step_fn``) so
+the orchestration is tested on CPU with gloo against the oracle (tests/test_dist.py).
+"""
+
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+from . import _lib
+
+
+@dataclass(frozen=True)
+class Layout:
+    rows: int  # R row groups
+    cols: int  # C column groups
+
+    @property
+    def size(self) -> int:
+        return self.rows * self.cols
+
+    def coords(self, rank: int):
+        """(row group, column group) of a rank; ranks of one column group are contiguous
+        in row order so that a column group's all-gather is a plain ordered all-gather."""
+        return rank % self.rows, rank // self.rows
+
+    @staticmethod
+    def parse(spec: str, world: int) -> "Layout":
+        if spec in ("row", "rows"):
+            return Layout(world, 1)
+        if spec in ("col", "cols", "column"):
+            return Layout(1, world)
+        r, c = (int(x) for x in spec.lower().split("x"))
+        if r * c != world:
+            raise ValueError(f"layout {spec} does not cover {world} ranks")
+        return Layout(r, c)
+
+
+def row_range(n: int, R: int, ri: int):
+    """Equal-size row shards (all_gather_into_tensor needs equal counts): shard = ceil(n/R);
+    the padded tail rows beyond n are never referenced by a column index."""
+    shard = -(-n // R) if R > 0 else n
+    lo = min(n, ri * shard)
+    hi = min(n, lo + shard)
+    return lo, hi, shard
+
+
+def col_range(f: int, C: int, ci: int):
+    base, rem = divmod(f, C)
+    lo = ci * base + min(ci, rem)
+    return lo, lo + base + (1 if ci < rem else 0)
+
+
+def line_ld(width: int, elem_bytes: int = 4) -> int:
+    """Leading dimension (elements) that keeps a row inside as few 128-B lines as possible:
+    the next power of two up to a line, then a multiple of the line."""
+    if width <= 0:
+        return 1
+    line = 128 // elem_bytes
+    if width <= line:
+        return 1 << (width - 1).bit_length()
+    return -(-width // line) * line
+
+
+class _TorchComm:
+    """In-place all-gather of equal row shards within a column group (RCCL for 'nccl')."""
+
+    def __init__(self, layout: Layout, rank: int):
+        self.layout = layout
+        self.groups = {}
+        ri, ci = layout.coords(rank)
+        self.ri, self.ci = ri, ci
+        if layout.rows > 1:
+            for c in range(layout.cols):
+                members = [c * layout.rows + r for r in range(layout.rows)]
+                g = dist.new_group(members) if layout.cols > 1 else None
+                if c == ci:
+                    self.group = g
+        self.backend = dist.get_backend() if dist.is_initialized() else None
+
+    def all_gather_rows(self, full: torch.Tensor, shard_rows: int, async_op: bool):
+        """full: [R * shard_rows, ld]; this rank's shard already sits at row ri*shard_rows."""
+        R = self.layout.rows
+        if R == 1:
+            return None
+        mine = full[self.ri * shard_rows:(self.ri + 1) * shard_rows]
+        if self.backend == "nccl":
+            return dist.all_gather_into_tensor(full, mine, group=self.group, async_op=async_op)
+        # gloo (CPU tests, single-GPU multi-process rehearsal): stage through host memory
+        host = full.detach().to("cpu", copy=True) if full.is_cuda else full
+        parts = list(host.split(shard_rows))
+        dist.all_gather(parts, parts[self.ri].clone(), group=self.group)
+        if full.is_cuda:
+            full.copy_(host)
+        return None
+
+
+class NullComm:
+    """No exchange (emulation of one rank on one GPU; the gathered rows keep stale data)."""
+
+    def all_gather_rows(self, full, shard_rows, async_op):
+        return None
+
+
+class PartitionedAPPNP:
+    """K-iteration APPNP over a Layout of ranks.  Build with :meth:`create`."""
+
+    def __init__(self, layout, rank, n, f, K, alpha, graph, H_slab, f_lo, f_hi, bufs, shard,
+                 lo, hi, comm, step_fn, overlap, partial, p_drop=0.0, seed=0):
+        self.layout, self.rank = layout, rank
+        self.n, self.f, self.K, self.alpha = n, f, K, alpha
+        self.graph = graph
+        self.H = H_slab
+        self.f_lo, self.f_hi = f_lo, f_hi
+        self.bufs = bufs
+        self.shard, self.lo, self.hi = shard, lo, hi
+        self.comm, self.step_fn = comm, step_fn
+        self.overlap, self.partial = overlap, partial
+        self.p_drop, self.seed = p_drop, seed
+        self.out = None
+
+    # -- construction ---------------------------------------------------------------------
+    @classmethod
+    def create(cls, indptr, indices, n, H, K, alpha, device, layout: Layout | None = None,
+               overlap=False, data=None, mode="sym", comm=None, step_fn=None, graph_fn=None,
+               p_drop=0.0, seed=0, rank=None, world=None):
+        """rank / world override the process group's (single-GPU emulation of one rank of a
+        larger layout, with a ``NullComm``: measures that rank's kernel time only)."""
+        if rank is None:
+            rank = dist.get_rank() if dist.is_initialized() else 0
+        if world is None:
+            world = dist.get_world_size() if dist.is_initialized() else 1
+        layout = layout or Layout(1, world)
+        if layout.size != world:
+            raise ValueError("layout does not match the world size")
+        ri, ci = layout.coords(rank)
+        f = int(H.shape[1])
+        lo, hi, shard = row_range(n, layout.rows, ri)
+        f_lo, f_hi = col_range(f, layout.cols, ci)
+        width = f_hi - f_lo
+        esz = H.element_size()
+        ld = line_ld(width, esz)
+        overlap = bool(overlap and layout.rows > 1)
+        if graph_fn is None:
+            from .graph import Graph
+
+            graph = Graph.from_csr(indptr, indices, data, n, mode=mode, device=device,
+                                   row_lo=lo, row_hi=hi, split_local=overlap)
+        else:
+            graph = graph_fn(lo, hi, overlap)
+        rows_pad = shard * layout.rows
+        H_slab = torch.zeros(max(hi - lo, 0), ld, dtype=H.dtype, device=device)
+        H_slab[:, :width] = H[lo:hi, f_lo:f_hi].to(device)
+        bufs = [torch.zeros(rows_pad, ld, dtype=H.dtype, device=device) for _ in range(2)]
+        partial = (torch.zeros(max(hi - lo, 0), ld, dtype=torch.float32, device=device)
+                   if overlap else None)
+        comm = comm or _TorchComm(layout, rank)
+        step_fn = step_fn or _hip_step
+        return cls(layout, rank, n, f, K, alpha, graph, H_slab, f_lo, f_hi, bufs, shard, lo, hi,
+                   comm, step_fn, overlap, partial, p_drop, seed)
+
+    @property
+    def nnz_hat_local(self) -> int:
+        return self.graph.nnz_hat
+
+    @property
+    def width(self) -> int:
+        return self.f_hi - self.f_lo
+
+    # -- the K loop -----------------------------------------------------------------------
+    def run(self):
+        """Z_K for this rank's rows x feature slab; returns a [hi-lo, width] view."""
+        K, R = self.K, self.layout.rows
+        w = self.width
+        lo, hi, shard = self.lo, self.hi, self.shard
+        if K == 0:
+            self.out = self.H[:, :w]
+            return self.out
+        # Z_0 = H: the full Z_0 needs every row shard of H (iteration 0 gathers from it)
+        cur = self.bufs[0]
+        cur[lo:hi].copy_(self.H)
+        work = self.comm.all_gather_rows(cur, shard, async_op=False) if R > 1 else None
+        if R == 1:
+            cur = None  # gather straight from H (all rows held)
+        nxt_i = 1
+        for k in range(K):
+            src = self.H if cur is None else cur
+            dst = self.bufs[nxt_i]
+            out_rows = dst[lo:hi]
+            if self.overlap:
+                # local columns first (ready before the all-gather of src completes)
+                self.step_fn(self, src, out_rows, k, _lib.PART_LOCAL)
+                if work is not None:
+                    work.wait()
+                    work = None
+                self.step_fn(self, src, out_rows, k, _lib.PART_REMOTE)
+            else:
+                if work is not None:
+                    work.wait()
+                    work = None
+                self.step_fn(self, src, out_rows, k, _lib.PART_ALL)
+            if k < K - 1 and R > 1:
+                # async (overlap) returns a work handle waited on inside the next iteration;
+                # sync collectives are stream-ordered and return None
+                work = self.comm.all_gather_rows(dst, shard, async_op=self.overlap)
+            cur = dst
+            nxt_i ^= 1
+        if work is not None:
+            work.wait()
+        self.out = cur[lo:hi, :w]
+        return self.out
+
+
+def _hip_step(runner: PartitionedAPPNP, src, out_rows, k, part):
+    """One iteration through the C ABI (appnp_step)."""
+    from .ops import step
+
+    w = runner.width
+    Zin = src[:, :w] if src.shape[0] == runner.graph.n else src[: runner.graph.n, :w]
+    H = runner.H[:, :w]
+    if part == _lib.PART_LOCAL:
+        step(runner.graph, Zin, None, runner.partial[:, :w], k, runner.alpha,
+             part=_lib.PART_LOCAL, p_drop=runner.p_drop, seed=runner.seed)
+    elif part == _lib.PART_REMOTE:
+        step(runner.graph, Zin, H, out_rows[:, :w], k, runner.alpha, part=_lib.PART_REMOTE,
+             partial=runner.partial[:, :w], p_drop=runner.p_drop, seed=runner.seed)
+    else:
+        step(runner.graph, Zin, H, out_rows[:, :w], k, runner.alpha, p_drop=runner.p_drop,
+             seed=runner.seed)
+
+
+def choose_layout(world: int, n: int, f: int, nnz: int, elem_bytes: int = 4) -> Layout:
+    """Default layout: the column partition (no data-path collective) unless F is too narrow
+    to split; see DESIGN.md 'Multi-GPU' for the line-request model behind it."""
+    if f >= world:
+        return Layout(1, world)
+    c = max(1, math.gcd(world, f))
+    return Layout(world // c, c)

@@ -1,0 +1,118 @@
+"""CPU, world_size 2 (gloo): the multi-GPU orchestration of ppnp_amd.dist against the oracle.
+
+The per-iteration kernel is replaced by an oracle step on the same CSR rows (the GPU kernel
+itself is covered by tests/test_gpu_parity.py); what is tested here is the layout, the row /
+feature slab bookkeeping, the equal-shard all-gather and the local/remote split of the
+overlap mode, for row, column and 2-D layouts.
+"""
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import ppnp_oracle as O
+
+N, F, K, ALPHA = 257, 10, 5, 0.15
+
+
+class _FakeGraph:
+    def __init__(self, a_hat, lo, hi, overlap):
+        self.n = a_hat.shape[0]
+        self.rows_csr = a_hat[lo:hi].tocsr()
+        self.nnz_hat = self.rows_csr.nnz
+        self.lo, self.hi = lo, hi
+        if overlap:
+            coo = self.rows_csr.tocoo()
+            loc = (coo.col >= lo) & (coo.col < hi)
+            shape = self.rows_csr.shape
+            self.local = sp.csr_matrix((coo.data[loc], (coo.row[loc], coo.col[loc])), shape=shape)
+            self.remote = sp.csr_matrix((coo.data[~loc], (coo.row[~loc], coo.col[~loc])),
+                                        shape=shape)
+
+
+def _oracle_step(runner, src, out_rows, k, part):
+    from ppnp_amd import _lib
+
+    g = runner.graph
+    w = runner.width
+    Zin = src[: g.n, :w].double().numpy()
+    H = runner.H[:, :w].double().numpy()
+    a = 1.0 - runner.alpha
+    if part == _lib.PART_LOCAL:
+        runner.partial[:, :w] = torch.from_numpy(a * (g.local @ Zin)).float()
+    elif part == _lib.PART_REMOTE:
+        y = a * (g.remote @ Zin) + runner.partial[:, :w].double().numpy() + runner.alpha * H
+        out_rows[:, :w] = torch.from_numpy(y).float()
+    else:
+        out_rows[:, :w] = torch.from_numpy(a * (g.rows_csr @ Zin) + runner.alpha * H).float()
+
+
+def _worker(rank, world, port, layout_spec, overlap, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from ppnp_amd.dist import Layout, PartitionedAPPNP
+
+        adj = O.synth_graph(N, 4 * N, seed=5)
+        a_hat = O.calc_a_hat(adj, "sym")
+        H = torch.randn(N, F, generator=torch.Generator().manual_seed(0))
+        layout = Layout.parse(layout_spec, world)
+        runner = PartitionedAPPNP.create(
+            None, None, N, H, K, ALPHA, "cpu", layout=layout, overlap=overlap,
+            graph_fn=lambda lo, hi, ov: _FakeGraph(a_hat, lo, hi, ov), step_fn=_oracle_step)
+        Z = runner.run()
+        ref = O.appnp_propagate(a_hat, H.numpy(), K, ALPHA)
+        sub = ref[runner.lo:runner.hi, runner.f_lo:runner.f_hi]
+        err = float(np.abs(Z.double().numpy() - sub).max()) if sub.size else 0.0
+        q.put((rank, runner.lo, runner.hi, runner.f_lo, runner.f_hi, err))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("layout,overlap", [("row", False), ("row", True), ("col", False),
+                                            ("1x2", False)])
+def test_partitioned_matches_oracle(layout, overlap):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    mp.start_processes(_worker, args=(world, _free_port(), layout, overlap, q), nprocs=world,
+                       join=True, start_method="spawn")
+    res = sorted(q.get() for _ in range(world))
+    covered = np.zeros((N, F), dtype=bool)
+    for rank, lo, hi, flo, fhi, err in res:
+        assert err < 1e-5, (rank, err)
+        covered[lo:hi, flo:fhi] = True
+    assert covered.all()  # every (row, feature) of Z_K is produced exactly by some rank
+
+
+def test_layout_helpers():
+    from ppnp_amd.dist import Layout, choose_layout, col_range, line_ld, row_range
+
+    assert Layout.parse("row", 8) == Layout(8, 1)
+    assert Layout.parse("col", 8) == Layout(1, 8)
+    assert Layout.parse("2x4", 8) == Layout(2, 4)
+    with pytest.raises(ValueError):
+        Layout.parse("3x3", 8)
+    spans = [row_range(10, 3, r) for r in range(3)]
+    assert spans == [(0, 4, 4), (4, 8, 4), (8, 10, 4)]
+    cols = [col_range(100, 8, c) for c in range(8)]
+    assert cols[0][0] == 0 and cols[-1][1] == 100
+    assert all(b - a in (12, 13) for a, b in cols)
+    assert line_ld(25) == 32 and line_ld(13) == 16 and line_ld(50) == 64 and line_ld(100) == 128
+    assert line_ld(7) == 8 and line_ld(40, 2) == 64
+    assert choose_layout(8, 2_449_029, 100, 126_000_000) == Layout(1, 8)

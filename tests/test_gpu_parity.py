@@ -306,3 +306,47 @@ def test_ppnp_and_appnp_logits(ds, request):
         out3 = ap(X.to(DEV), idx=None, ppr=sub).cpu().numpy()
     ref3 = g["ppnp_logits_ppr_mode"]
     assert np.abs(out3 - ref3).max() <= 1e-4 * np.abs(ref3).max()
+
+
+# ---------------------------------------------------------------------------------------
+# row-partitioned step (multi-GPU building block): held rows, local/remote split
+# ---------------------------------------------------------------------------------------
+
+
+@pytest.mark.parametrize("lo,hi", [(0, 700), (700, 1400), (1400, 2000), (0, 2000)])
+def test_step_rows_and_split(lo, hi):
+    pa = _lib()
+    from ppnp_amd import _lib as L
+
+    n, F = 2000, 24
+    adj = synth(n, 9000, seed=21)
+    ah = O.calc_a_hat(adj, "sym")
+    Zin = torch.randn(n, F, generator=torch.Generator().manual_seed(1))
+    H = torch.randn(hi - lo, F, generator=torch.Generator().manual_seed(2))
+    ref = 0.8 * (ah[lo:hi] @ Zin.double().numpy()) + 0.2 * H.double().numpy()
+    G = pa.Graph.from_scipy(adj, device=DEV, row_lo=lo, row_hi=hi, split_local=True)
+    assert G.rows == hi - lo and G.n == n
+    out = torch.empty(hi - lo, F, device=DEV)
+    pa.step(G, Zin.to(DEV), H.to(DEV), out, 0, 0.2)
+    close_fp32(to_np(out), ref)
+    part = torch.empty(hi - lo, F, device=DEV)
+    out2 = torch.empty(hi - lo, F, device=DEV)
+    pa.step(G, Zin.to(DEV), None, part, 0, 0.2, part=L.PART_LOCAL)
+    pa.step(G, Zin.to(DEV), H.to(DEV), out2, 0, 0.2, part=L.PART_REMOTE, partial=part)
+    close_fp32(to_np(out2), ref)
+
+
+def test_step_dropout_uses_global_row_keys():
+    """A row shard applies the same mask as the full graph (key = global (row, col))."""
+    pa = _lib()
+    n, F, lo, hi = 1500, 8, 600, 1100
+    adj = synth(n, 6000, seed=4)
+    Zin = torch.randn(n, F, generator=torch.Generator().manual_seed(3)).to(DEV)
+    H = torch.randn(n, F, generator=torch.Generator().manual_seed(4)).to(DEV)
+    Gfull = pa.Graph.from_scipy(adj, device=DEV)
+    Gpart = pa.Graph.from_scipy(adj, device=DEV, row_lo=lo, row_hi=hi)
+    full = torch.empty(n, F, device=DEV)
+    part = torch.empty(hi - lo, F, device=DEV)
+    pa.step(Gfull, Zin, H, full, 3, 0.1, p_drop=0.4, seed=99)
+    pa.step(Gpart, Zin, H[lo:hi], part, 3, 0.1, p_drop=0.4, seed=99)
+    assert torch.equal(full[lo:hi], part)
