@@ -32,6 +32,7 @@ import torch  # noqa: E402
 import helpers  # noqa: E402  (reference)
 import model  # noqa: E402  (reference)
 from ppnp.data.sparsegraph import SparseGraph  # noqa: E402  (reference)
+from ppnp.preprocessing import gen_splits, normalize_attributes  # noqa: E402  (reference)
 
 
 def load_raw(name):
@@ -116,6 +117,18 @@ def dataset(name, with_attr):
     out["ppnp_logits"] = logits.numpy()
     out["ppnp_logits_ppr_mode"] = logits_ppr_mode.numpy()
 
+    # preprocessing.py:9-64 -- splits for two seeds (main.py:84-98 call pattern), L1 norm
+    for tag, sd in (("a", 2413340114), ("b", 123456789)):
+        args = {"ntrain_per_class": 20, "nstopping": 500, "nknown": 1500, "seed": sd}
+        tr, st, va = gen_splits(g.labels, args, test=False)
+        _, _, te = gen_splits(g.labels, args, test=True)
+        out[f"split_{tag}_seed"] = np.int64(sd)
+        out[f"split_{tag}_train"] = np.asarray(tr, dtype=np.int64)
+        out[f"split_{tag}_stop"] = np.asarray(st, dtype=np.int64)
+        out[f"split_{tag}_valid"] = np.asarray(va, dtype=np.int64)
+        out[f"split_{tag}_test"] = np.asarray(te, dtype=np.int64)
+    xn = normalize_attributes(g.attr_matrix)
+    out["attr_l1_rowsum"] = np.asarray(abs(xn).sum(axis=1)).ravel().astype(np.float64)
     if with_attr:
         at = csr_sorted(g.attr_matrix)
         out["attr_indptr"] = at.indptr.astype(np.int32)
@@ -165,4 +178,4 @@ def kats():
 if __name__ == "__main__":
     kats()
     dataset("cora_ml", with_attr=True)
-    dataset("citeseer", with_attr=False)
+    dataset("citeseer", with_attr=True)
