@@ -34,6 +34,9 @@ sys.path.insert(0, ROOT)
 
 METRIC = "APPNP K=10 propagated node-feats/sec; achieved HBM GB/s vs peak, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip-level parameters)
+# random row-gather ceiling measured on MI355X: ~54-57 G cache-line requests/s for 64-512 B
+# rows from a 1 GB table (profiles/r1_gather_probe.txt)
+GATHER_LINE_CEILING = 56.0
 
 
 def parse():
@@ -42,6 +45,8 @@ def parse():
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--workload", default="products-synth")
+    p.add_argument("--dtype", default=None, choices=["f32", "bf16"],
+                   help="override the workload's storage dtype (non-headline variants)")
     p.add_argument("--cpu-iters", type=int, default=2,
                    help="iterations of the CPU baseline sample (0 disables it)")
     p.add_argument("--layout", default="auto",
@@ -52,6 +57,17 @@ def parse():
     p.add_argument("--overlap", action="store_true",
                    help="row layouts: overlap the all-gather with the local-column product")
     return p.parse_args()
+
+
+def committed_traffic(workload, dtype, parallelism):
+    """HBM bytes per launch of the SpMM kernel from the committed PMC profile of the same
+    command (tools/summarize_profile.py writes profiles/pmc_traffic.json), or None."""
+    key = f"{workload}:{'bf16' if dtype == torch.bfloat16 else 'f32'}:{parallelism}"
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as fh:
+            return json.load(fh).get(key)
+    except (OSError, ValueError):
+        return None
 
 
 def log(*a):
@@ -99,6 +115,8 @@ def main():
     from ppnp_amd import dist as pdist
 
     n, m, F, K, alpha, dtype = synth.CONFIGS[args.workload]
+    if args.dtype:
+        dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     seed = synth.SEEDS.get(args.workload, 0)
     distributed = world > 1 or args.layout != "auto"
     emu = {}
@@ -122,6 +140,12 @@ def main():
     t0 = time.perf_counter()
     indptr, indices = synth.uniform_graph_device(n, m, seed, device=dev)
     H = synth.features(n, F, dtype=dtype, device=dev)
+    esz = 2 if dtype == torch.bfloat16 else 4
+    ld = pdist.line_ld(F, esz)
+    if ld != F:  # line-aligned rows; H/Z are [N, F] views of [N, ld] buffers
+        Hbuf = torch.zeros(n, ld, dtype=dtype, device=dev)
+        Hbuf[:, :F] = H
+        H = Hbuf[:, :F]
     torch.cuda.synchronize()
     t_gen = time.perf_counter() - t0
 
@@ -145,7 +169,7 @@ def main():
         graph = ppnp_amd.Graph.from_csr(indptr, indices, None, n, mode="sym", device=dev)
         torch.cuda.synchronize()
         t_build = time.perf_counter() - t1
-        Z = torch.empty_like(H)
+        Z = torch.empty(n, ld, dtype=dtype, device=dev)[:, :F]
 
         def run():
             ppnp_amd.propagate_forward(graph, H, K, alpha, out=Z)
@@ -190,7 +214,16 @@ def main():
     b_iter = 4 * (rows_local + 1) + 8 * nnz_local + 3 * rows_local * F_local * s
     avg_launch_ms = dev_ms / (args.steps * K)
     achieved = b_iter / (avg_launch_ms * 1e-3) / 1e9
+    # gather line-request rate: every nonzero gathers one row of Z_k
+    ld_l = pdist.line_ld(F_local, s)
+    lines_per_row = 1 if ld_l * s <= 128 else -(-(F_local * s) // 128)
+    lines = nnz_local * lines_per_row + (8 * nnz_local + 3 * rows_local * ld_l * s) / 128
+    line_rate = lines / (avg_launch_ms * 1e-3) / 1e9
     value = n * F * K * args.steps / wall
+    parallelism = ((f"rows{runner.layout.rows}xcols{runner.layout.cols}"
+                    + ("-overlap" if args.overlap else "")
+                    + (f"-EMULATED-rank{args.emulate}" if args.emulate else ""))
+                   if distributed else "single")
     res = {
         "metric": METRIC,
         "value": value,
@@ -213,10 +246,7 @@ def main():
             "K": K,
             "alpha": alpha,
             "norm": "sym",
-            "parallelism": (f"rows{runner.layout.rows}xcols{runner.layout.cols}"
-                            + ("-overlap" if args.overlap else "")
-                            + (f"-EMULATED-rank{args.emulate}" if args.emulate else ""))
-                           if distributed else "single",
+            "parallelism": parallelism,
         },
         "roofline": {
             "bound": "hbm",
@@ -224,7 +254,16 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
-            "traffic": None,
+            "traffic": committed_traffic(args.workload, dtype, parallelism),
+            "traffic_source": "profiles/pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE / "
+                              "WRITE_SIZE passes of this bench command, gfx950-corrected)",
+            "gather_line_rate": {
+                "lines_per_launch": lines,
+                "achieved_G_lines_s": line_rate,
+                "ceiling_G_lines_s": GATHER_LINE_CEILING,
+                "frac": line_rate / GATHER_LINE_CEILING,
+                "ceiling_source": "tools/gather_probe.hip, profiles/r1_gather_probe.txt",
+            },
             "kernel": "k_step_wide (one launch per iteration)",
             "bytes_per_launch": b_iter,
             "avg_launch_ms": avg_launch_ms,

@@ -99,7 +99,9 @@ int appnp_graph_copy_csr(const appnp_graph* g, int32_t* row_ptr, int32_t* col, f
 /* Device view of the fp64 inverse-degree vector (1/sqrt(D) for sym, 1/D for rw), length n. */
 int appnp_graph_dinv(const appnp_graph* g, const double** dinv);
 
-/* Bytes of workspace appnp_propagate / appnp_propagate_bwd need for this shape. */
+/* Bytes of workspace appnp_propagate / appnp_propagate_bwd need for this shape.  The
+ * workspace holds the ping-pong iterates with its own line-aligned leading dimension
+ * (`ld` is accepted for ABI stability and ignored). */
 size_t appnp_workspace_bytes(const appnp_graph* g, int64_t f, int64_t ld, int dtype);
 
 /*

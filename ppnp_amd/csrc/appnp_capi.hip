@@ -25,6 +25,20 @@ inline int64_t elem_size(int dtype) { return dtype == APPNP_F32 ? 4 : 2; }
 
 inline bool valid_dtype(int dtype) { return dtype == APPNP_F32 || dtype == APPNP_BF16; }
 
+// Leading dimension of the internal ping-pong buffers: a row starts on a 128-B line and
+// spans as few lines as possible (next power of two up to one line, then whole lines).
+// A random row gather costs cache-line requests, not bytes.
+inline int64_t line_ld(int64_t f, int dtype) {
+  const int64_t line = 128 / elem_size(dtype);
+  if (f <= 0) return 1;
+  if (f <= line) {
+    int64_t p = 1;
+    while (p < f) p <<= 1;
+    return p;
+  }
+  return (f + line - 1) / line * line;
+}
+
 // Per-iteration dropout parameters (identical to oracle/ppnp_oracle.py edge_keep_mask).
 void set_drop(StepArgs& a, float p_drop, uint64_t seed, int k) {
   if (p_drop > 0.0f) {
@@ -159,10 +173,10 @@ int appnp_graph_dinv(const appnp_graph* g, const double** dinv) {
 
 size_t appnp_workspace_bytes(const appnp_graph* g, int64_t f, int64_t ld, int dtype) {
   if (!g || f < 0 || !valid_dtype(dtype)) return 0;
-  if (ld < f) ld = f;
+  (void)ld;  // the workspace uses its own line-aligned leading dimension
   const int64_t rows = g->row_hi - g->row_lo;
-  // two ping-pong buffers (the forward needs one, the adjoint two)
-  return (size_t)(2 * rows * ld * elem_size(dtype));
+  // two ping-pong buffers (the forward needs one, the adjoint two), 256-B aligned
+  return (size_t)(2 * rows * line_ld(f, dtype) * elem_size(dtype) + 256);
 }
 
 int appnp_propagate(const appnp_graph* g, const void* H, int64_t ld_h, void* Z, int64_t ld_z,
@@ -179,9 +193,13 @@ int appnp_propagate(const appnp_graph* g, const void* H, int64_t ld_h, void* Z, 
   if (K == 0)
     return dev_err(hipMemcpy2DAsync(Z, ld_z * es, H, ld_h * es, f * es, n,
                                     hipMemcpyDeviceToDevice, s));
-  const int64_t ld_w = ld_z;
+  const int64_t ld_w = line_ld(f, dtype);
   if (K >= 2) {
-    if (!ws || ws_bytes < (size_t)(n * ld_w * es)) return APPNP_EINVAL;
+    if (!ws) return APPNP_EINVAL;
+    const uintptr_t base = reinterpret_cast<uintptr_t>(ws);
+    const uintptr_t aligned = (base + 255) & ~uintptr_t(255);
+    if (ws_bytes < (size_t)(n * ld_w * es) + (aligned - base)) return APPNP_EINVAL;
+    ws = reinterpret_cast<void*>(aligned);
   }
   const int64_t lds[3] = {ld_h, ld_z, ld_w};
   const void* ptrs[3] = {H, Z, K >= 2 ? ws : nullptr};
@@ -226,10 +244,16 @@ int appnp_propagate_bwd(const appnp_graph* g, const void* dZ, int64_t ld_dz, voi
   if (K == 0)
     return dev_err(hipMemcpy2DAsync(dH, ld_dh * es, dZ, ld_dz * es, f * es, n,
                                     hipMemcpyDeviceToDevice, s));
-  const int64_t ld_w = ld_dh;
+  const int64_t ld_w = line_ld(f, dtype);
   const int64_t buf = n * ld_w * es;
   const int nbuf = K >= 3 ? 2 : (K == 2 ? 1 : 0);
-  if (nbuf > 0 && (!ws || ws_bytes < (size_t)(nbuf * buf))) return APPNP_EINVAL;
+  if (nbuf > 0) {
+    if (!ws) return APPNP_EINVAL;
+    const uintptr_t base = reinterpret_cast<uintptr_t>(ws);
+    const uintptr_t aligned = (base + 255) & ~uintptr_t(255);
+    if (ws_bytes < (size_t)(nbuf * buf) + (aligned - base)) return APPNP_EINVAL;
+    ws = reinterpret_cast<void*>(aligned);
+  }
   void* w0 = ws;
   void* w1 = nbuf == 2 ? static_cast<char*>(ws) + buf : nullptr;
   const int64_t lds[3] = {ld_dz, ld_dh, ld_w};

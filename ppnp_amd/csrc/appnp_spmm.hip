@@ -28,39 +28,122 @@ namespace appnp {
 
 namespace {
 
-template <typename T, int V, int EPI>
+// ---- row fragments: V consecutive elements at p.  With TAIL, a lane whose fragment crosses
+// the end of the row (rem = f - col0 < V valid elements) reads/writes exactly those rem
+// elements, in descending power-of-two pieces at compile-time offsets (no over-read past F,
+// no runtime register indexing).  All tail lanes of a wave share rem, so the switch is
+// wave-uniform.
+template <typename T, int N, int O, int V>
+__device__ __forceinline__ void ld_at(const T* p, float (&x)[V]) {
+  float t[N];
+  Io<T, N>::load(p + O, t);
+#pragma unroll
+  for (int i = 0; i < N; ++i) x[O + i] = t[i];
+}
+
+template <typename T, int N, int O, int V>
+__device__ __forceinline__ void st_at(T* p, const float (&x)[V]) {
+  float t[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) t[i] = x[O + i];
+  Io<T, N>::store(p + O, t);
+}
+
+template <typename T, int V, bool TAIL>
+__device__ __forceinline__ void frag_load(const T* p, float (&x)[V], int rem) {
+  if (!TAIL || rem >= V) {
+    Io<T, V>::load(p, x);
+    return;
+  }
+#pragma unroll
+  for (int v = 0; v < V; ++v) x[v] = 0.0f;
+  if constexpr (V == 8) {
+    switch (rem) {
+      case 1: ld_at<T, 1, 0>(p, x); break;
+      case 2: ld_at<T, 2, 0>(p, x); break;
+      case 3: ld_at<T, 2, 0>(p, x); ld_at<T, 1, 2>(p, x); break;
+      case 4: ld_at<T, 4, 0>(p, x); break;
+      case 5: ld_at<T, 4, 0>(p, x); ld_at<T, 1, 4>(p, x); break;
+      case 6: ld_at<T, 4, 0>(p, x); ld_at<T, 2, 4>(p, x); break;
+      case 7: ld_at<T, 4, 0>(p, x); ld_at<T, 2, 4>(p, x); ld_at<T, 1, 6>(p, x); break;
+      default: break;
+    }
+  } else if constexpr (V == 4) {
+    switch (rem) {
+      case 1: ld_at<T, 1, 0>(p, x); break;
+      case 2: ld_at<T, 2, 0>(p, x); break;
+      case 3: ld_at<T, 2, 0>(p, x); ld_at<T, 1, 2>(p, x); break;
+      default: break;
+    }
+  } else if constexpr (V == 2) {
+    if (rem == 1) ld_at<T, 1, 0>(p, x);
+  }
+}
+
+template <typename T, int V, bool TAIL>
+__device__ __forceinline__ void frag_store(T* p, const float (&x)[V], int rem) {
+  if (!TAIL || rem >= V) {
+    Io<T, V>::store(p, x);
+    return;
+  }
+  if constexpr (V == 8) {
+    switch (rem) {
+      case 1: st_at<T, 1, 0>(p, x); break;
+      case 2: st_at<T, 2, 0>(p, x); break;
+      case 3: st_at<T, 2, 0>(p, x); st_at<T, 1, 2>(p, x); break;
+      case 4: st_at<T, 4, 0>(p, x); break;
+      case 5: st_at<T, 4, 0>(p, x); st_at<T, 1, 4>(p, x); break;
+      case 6: st_at<T, 4, 0>(p, x); st_at<T, 2, 4>(p, x); break;
+      case 7: st_at<T, 4, 0>(p, x); st_at<T, 2, 4>(p, x); st_at<T, 1, 6>(p, x); break;
+      default: break;
+    }
+  } else if constexpr (V == 4) {
+    switch (rem) {
+      case 1: st_at<T, 1, 0>(p, x); break;
+      case 2: st_at<T, 2, 0>(p, x); break;
+      case 3: st_at<T, 2, 0>(p, x); st_at<T, 1, 2>(p, x); break;
+      default: break;
+    }
+  } else if constexpr (V == 2) {
+    if (rem == 1) st_at<T, 1, 0>(p, x);
+  }
+}
+
+template <typename T, int V, int EPI, bool TAIL>
 __device__ __forceinline__ void epilogue(const StepArgs& a, int64_t row, int col0,
-                                         const float (&acc)[V], const float (&hv)[V]) {
+                                         const float (&acc)[V], const float (&hv)[V],
+                                         int rem) {
   float y[V];
 #pragma unroll
   for (int v = 0; v < V; ++v) y[v] = a.scale * acc[v];
   if constexpr (EPI == EPI_FWD) {
 #pragma unroll
     for (int v = 0; v < V; ++v) y[v] = fmaf(a.alpha, hv[v], y[v]);
-    Io<T, V>::store(static_cast<T*>(a.out) + row * a.ld_out + col0, y);
+    frag_store<T, V, TAIL>(static_cast<T*>(a.out) + row * a.ld_out + col0, y, rem);
   } else if constexpr (EPI == EPI_BWD) {
-    if (a.out) Io<T, V>::store(static_cast<T*>(a.out) + row * a.ld_out + col0, y);
+    if (a.out) frag_store<T, V, TAIL>(static_cast<T*>(a.out) + row * a.ld_out + col0, y, rem);
     T* d = static_cast<T*>(a.aux) + row * a.ld_aux + col0;
     float dv[V];
-    Io<T, V>::load(d, dv);
+    frag_load<T, V, TAIL>(d, dv, rem);
 #pragma unroll
     for (int v = 0; v < V; ++v) dv[v] = fmaf(a.alpha, y[v], dv[v]);
-    Io<T, V>::store(d, dv);
+    frag_store<T, V, TAIL>(d, dv, rem);
   } else if constexpr (EPI == EPI_PARTIAL) {
-    Io<float, V>::store(static_cast<float*>(a.out) + row * a.ld_out + col0, y);
+    frag_store<float, V, TAIL>(static_cast<float*>(a.out) + row * a.ld_out + col0, y, rem);
   } else {  // EPI_FINISH
     float pv[V];
-    Io<float, V>::load(static_cast<const float*>(a.aux) + row * a.ld_aux + col0, pv);
+    frag_load<float, V, TAIL>(static_cast<const float*>(a.aux) + row * a.ld_aux + col0, pv, rem);
 #pragma unroll
     for (int v = 0; v < V; ++v) y[v] = fmaf(a.alpha, hv[v], y[v] + pv[v]);
-    Io<T, V>::store(static_cast<T*>(a.out) + row * a.ld_out + col0, y);
+    frag_store<T, V, TAIL>(static_cast<T*>(a.out) + row * a.ld_out + col0, y, rem);
   }
 }
 
-template <typename T, int V, int EPI>
-__device__ __forceinline__ void load_h(const StepArgs& a, int64_t row, int col0, float (&hv)[V]) {
+template <typename T, int V, int EPI, bool TAIL>
+__device__ __forceinline__ void load_h(const StepArgs& a, int64_t row, int col0, float (&hv)[V],
+                                       int rem) {
   if constexpr (EPI == EPI_FWD || EPI == EPI_FINISH) {
-    Io<T, V>::load(static_cast<const T*>(a.h) + row * a.ld_h + col0, hv);
+    frag_load<T, V, TAIL>(static_cast<const T*>(a.h) + row * a.ld_h + col0, hv, rem);
   } else {
 #pragma unroll
     for (int v = 0; v < V; ++v) hv[v] = 0.0f;
@@ -70,7 +153,7 @@ __device__ __forceinline__ void load_h(const StepArgs& a, int64_t row, int col0,
 // ------------------------------------------------------------------------------------------
 // wide: one wavefront per row, P = 64/G sub-groups split the row's entries
 // ------------------------------------------------------------------------------------------
-template <typename T, int V, int G, int EPI, int U>
+template <typename T, int V, int G, int EPI, int U, bool TAIL>
 __global__ __launch_bounds__(kBlock) void k_step_wide(StepArgs a) {
   constexpr int P = kWave / G;
   __shared__ int2 stage[kWavesPerBlock][kWave];
@@ -79,7 +162,8 @@ __global__ __launch_bounds__(kBlock) void k_step_wide(StepArgs a) {
   const int sub = lane / G;
   const int gl = lane % G;
   const int col0 = blockIdx.y * (G * V) + gl * V;
-  const bool fact = col0 < a.f;
+  const int rem = a.f - col0;  // valid features of this lane's fragment (>= V: full)
+  const bool fact = rem > 0;
   const T* __restrict__ zin = static_cast<const T*>(a.zin);
   int2* tile = stage[wave];
   const int64_t nwaves = (int64_t)gridDim.x * kWavesPerBlock;
@@ -88,7 +172,7 @@ __global__ __launch_bounds__(kBlock) void k_step_wide(StepArgs a) {
     const int beg = a.row_ptr[row];
     const int end = a.row_ptr[row + 1];
     float hv[V];
-    if (sub == 0 && fact) load_h<T, V, EPI>(a, row, col0, hv);
+    if (sub == 0 && fact) load_h<T, V, EPI, TAIL>(a, row, col0, hv, rem);
     float acc[V];
 #pragma unroll
     for (int v = 0; v < V; ++v) acc[v] = 0.0f;
@@ -114,7 +198,7 @@ __global__ __launch_bounds__(kBlock) void k_step_wide(StepArgs a) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           if (fact && t + u * P < n) {
-            Io<T, V>::load(zin + (int64_t)e[u].x * a.ld_in + col0, z[u]);
+            frag_load<T, V, TAIL>(zin + (int64_t)e[u].x * a.ld_in + col0, z[u], rem);
           } else {
 #pragma unroll
             for (int v = 0; v < V; ++v) z[u][v] = 0.0f;
@@ -135,14 +219,14 @@ __global__ __launch_bounds__(kBlock) void k_step_wide(StepArgs a) {
 #pragma unroll
       for (int v = 0; v < V; ++v) acc[v] += __shfl_xor(acc[v], off);
     }
-    if (sub == 0 && fact) epilogue<T, V, EPI>(a, row, col0, acc, hv);
+    if (sub == 0 && fact) epilogue<T, V, EPI, TAIL>(a, row, col0, acc, hv, rem);
   }
 }
 
 // ------------------------------------------------------------------------------------------
 // narrow: one G-lane group per row, P = 64/G rows per wave
 // ------------------------------------------------------------------------------------------
-template <typename T, int V, int G, int EPI, int U>
+template <typename T, int V, int G, int EPI, int U, bool TAIL>
 __global__ __launch_bounds__(kBlock) void k_step_narrow(StepArgs a) {
   constexpr int P = kWave / G;
   const int lane = threadIdx.x & (kWave - 1);
@@ -150,7 +234,8 @@ __global__ __launch_bounds__(kBlock) void k_step_narrow(StepArgs a) {
   const int sub = lane / G;
   const int gl = lane % G;
   const int col0 = blockIdx.y * (G * V) + gl * V;
-  const bool fact = col0 < a.f;
+  const int rem = a.f - col0;  // valid features of this lane's fragment (>= V: full)
+  const bool fact = rem > 0;
   const T* __restrict__ zin = static_cast<const T*>(a.zin);
   const int64_t stride = (int64_t)gridDim.x * kWavesPerBlock * P;
 
@@ -161,7 +246,7 @@ __global__ __launch_bounds__(kBlock) void k_step_narrow(StepArgs a) {
     const int beg = a.row_ptr[row];
     const int end = a.row_ptr[row + 1];
     float hv[V];
-    if (fact) load_h<T, V, EPI>(a, row, col0, hv);
+    if (fact) load_h<T, V, EPI, TAIL>(a, row, col0, hv, rem);
     float acc[V];
 #pragma unroll
     for (int v = 0; v < V; ++v) acc[v] = 0.0f;
@@ -182,7 +267,7 @@ __global__ __launch_bounds__(kBlock) void k_step_narrow(StepArgs a) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if (fact && e + u < end) {
-          Io<T, V>::load(zin + (int64_t)c[u] * a.ld_in + col0, z[u]);
+          frag_load<T, V, TAIL>(zin + (int64_t)c[u] * a.ld_in + col0, z[u], rem);
         } else {
 #pragma unroll
           for (int v = 0; v < V; ++v) z[u][v] = 0.0f;
@@ -194,23 +279,23 @@ __global__ __launch_bounds__(kBlock) void k_step_narrow(StepArgs a) {
         for (int v = 0; v < V; ++v) acc[v] = fmaf(w[u], z[u][v], acc[v]);
       }
     }
-    if (fact) epilogue<T, V, EPI>(a, row, col0, acc, hv);
+    if (fact) epilogue<T, V, EPI, TAIL>(a, row, col0, acc, hv, rem);
   }
 }
 
-template <typename T, int V, int EPI>
+template <typename T, int V, int EPI, bool TAIL>
 hipError_t launch_g(int G, dim3 grid, const StepArgs& a, hipStream_t s) {
   constexpr int UW = 4;  // entries in flight per sub-group (wide)
   constexpr int UN = 4;  // entries in flight per row (narrow)
   const dim3 block(kBlock);
   switch (G) {
-    case 1: hipLaunchKernelGGL((k_step_narrow<T, V, 1, EPI, UN>), grid, block, 0, s, a); break;
-    case 2: hipLaunchKernelGGL((k_step_narrow<T, V, 2, EPI, UN>), grid, block, 0, s, a); break;
-    case 4: hipLaunchKernelGGL((k_step_narrow<T, V, 4, EPI, UN>), grid, block, 0, s, a); break;
-    case 8: hipLaunchKernelGGL((k_step_narrow<T, V, 8, EPI, UN>), grid, block, 0, s, a); break;
-    case 16: hipLaunchKernelGGL((k_step_wide<T, V, 16, EPI, UW>), grid, block, 0, s, a); break;
-    case 32: hipLaunchKernelGGL((k_step_wide<T, V, 32, EPI, UW>), grid, block, 0, s, a); break;
-    case 64: hipLaunchKernelGGL((k_step_wide<T, V, 64, EPI, UW>), grid, block, 0, s, a); break;
+    case 1: hipLaunchKernelGGL((k_step_narrow<T, V, 1, EPI, UN, TAIL>), grid, block, 0, s, a); break;
+    case 2: hipLaunchKernelGGL((k_step_narrow<T, V, 2, EPI, UN, TAIL>), grid, block, 0, s, a); break;
+    case 4: hipLaunchKernelGGL((k_step_narrow<T, V, 4, EPI, UN, TAIL>), grid, block, 0, s, a); break;
+    case 8: hipLaunchKernelGGL((k_step_narrow<T, V, 8, EPI, UN, TAIL>), grid, block, 0, s, a); break;
+    case 16: hipLaunchKernelGGL((k_step_wide<T, V, 16, EPI, UW, TAIL>), grid, block, 0, s, a); break;
+    case 32: hipLaunchKernelGGL((k_step_wide<T, V, 32, EPI, UW, TAIL>), grid, block, 0, s, a); break;
+    case 64: hipLaunchKernelGGL((k_step_wide<T, V, 64, EPI, UW, TAIL>), grid, block, 0, s, a); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -218,12 +303,17 @@ hipError_t launch_g(int G, dim3 grid, const StepArgs& a, hipStream_t s) {
 
 template <typename T, int EPI>
 hipError_t launch_v(int V, int G, dim3 grid, const StepArgs& a, hipStream_t s) {
+  const bool tail = (a.f % V) != 0;
   switch (V) {
-    case 1: return launch_g<T, 1, EPI>(G, grid, a, s);
-    case 2: return launch_g<T, 2, EPI>(G, grid, a, s);
-    case 4: return launch_g<T, 4, EPI>(G, grid, a, s);
+    case 1: return launch_g<T, 1, EPI, false>(G, grid, a, s);
+    case 2: return tail ? launch_g<T, 2, EPI, true>(G, grid, a, s)
+                        : launch_g<T, 2, EPI, false>(G, grid, a, s);
+    case 4: return tail ? launch_g<T, 4, EPI, true>(G, grid, a, s)
+                        : launch_g<T, 4, EPI, false>(G, grid, a, s);
     case 8:
-      if constexpr (sizeof(T) == 2) return launch_g<T, 8, EPI>(G, grid, a, s);
+      if constexpr (sizeof(T) == 2)
+        return tail ? launch_g<T, 8, EPI, true>(G, grid, a, s)
+                    : launch_g<T, 8, EPI, false>(G, grid, a, s);
       return hipErrorInvalidValue;
     default: return hipErrorInvalidValue;
   }
@@ -231,14 +321,16 @@ hipError_t launch_v(int V, int G, dim3 grid, const StepArgs& a, hipStream_t s) {
 
 }  // namespace
 
-// Largest vector width (elements) valid for every operand: F, all leading dims and all
-// base pointers must be multiples of V elements.
+// Largest vector width (elements) valid for every operand: all leading dims and all base
+// pointers must be multiples of V elements.  F need not be: the lane holding the last
+// fragment of a row then touches only the valid elements (TAIL kernels).  A vector wider
+// than F itself is never chosen.
 int pick_vec(int dtype, int64_t f, const int64_t* lds, int n_ld, const void* const* ptrs,
              int n_ptr) {
   const int es = dtype == 0 ? 4 : 2;
   int v = dtype == 0 ? 4 : 8;
   for (; v > 1; v >>= 1) {
-    bool ok = (f % v) == 0;
+    bool ok = v <= f || (f % v) == 0;
     for (int i = 0; i < n_ld && ok; ++i) ok = (lds[i] % v) == 0;
     for (int i = 0; i < n_ptr && ok; ++i)
       ok = ptrs[i] == nullptr || (reinterpret_cast<uintptr_t>(ptrs[i]) % (uintptr_t)(v * es)) == 0;
@@ -260,7 +352,8 @@ hipError_t launch_step(int dtype, int epi, int V, const StepArgs& a, hipStream_t
   while (G < lanes_needed) G <<= 1;
   const int64_t slabs = (a.f + (int64_t)G * V - 1) / ((int64_t)G * V);
   const int64_t rows_per_block = G >= 16 ? kWavesPerBlock : (int64_t)kWavesPerBlock * (kWave / G);
-  static const int max_blocks = env_int("APPNP_MAX_BLOCKS", 256 * 8);
+  // one wave per row (wide) by default: measured best on products-synth (tools/tune.sh)
+  static const int max_blocks = env_int("APPNP_MAX_BLOCKS", 1 << 30);
   int64_t blocks = (a.n_rows + rows_per_block - 1) / rows_per_block;
   if (blocks > max_blocks) blocks = max_blocks;
   const dim3 grid((unsigned)blocks, (unsigned)slabs);

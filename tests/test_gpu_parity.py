@@ -350,3 +350,42 @@ def test_step_dropout_uses_global_row_keys():
     pa.step(Gfull, Zin, H, full, 3, 0.1, p_drop=0.4, seed=99)
     pa.step(Gpart, Zin, H[lo:hi], part, 3, 0.1, p_drop=0.4, seed=99)
     assert torch.equal(full[lo:hi], part)
+
+
+# ---------------------------------------------------------------------------------------
+# vector tails: F not a multiple of the 16-B vector, padded rows; padding never read/written
+# ---------------------------------------------------------------------------------------
+
+
+@pytest.mark.parametrize("dtype,F,ld", [(torch.float32, 30, 32), (torch.float32, 7, 8),
+                                        (torch.float32, 101, 128), (torch.bfloat16, 100, 128),
+                                        (torch.bfloat16, 15, 16), (torch.bfloat16, 3, 8),
+                                        (torch.bfloat16, 13, 16), (torch.bfloat16, 70, 72)])
+def test_tail_fragments(dtype, F, ld):
+    pa = _lib()
+    n = 2500
+    adj = synth(n, 12000, seed=F)
+    G = pa.Graph.from_scipy(adj, device=DEV)
+    Hc = torch.randn(n, F, generator=torch.Generator().manual_seed(F)).to(dtype)
+    Hbuf = torch.full((n, ld), float("nan"), dtype=dtype, device=DEV)
+    Hbuf[:, :F] = Hc.to(DEV)
+    Zbuf = torch.full((n, ld), float("nan"), dtype=dtype, device=DEV)
+    pa.propagate_forward(G, Hbuf[:, :F], 7, 0.1, out=Zbuf[:, :F])
+    assert torch.isnan(Zbuf[:, F:]).all()          # padding not written
+    Z = to_np(Zbuf[:, :F])
+    assert np.isfinite(Z).all()                   # padding (NaN) never read into results
+    ref = O.appnp_propagate(O.calc_a_hat(adj, "sym"), Hc.float().numpy(), 7, 0.1)
+    if dtype == torch.float32:
+        close_fp32(Z, ref)
+    else:
+        assert np.abs(Z - ref).max() <= 2e-2 * np.abs(ref).max()
+
+
+def test_bf16_backward():
+    pa = _lib()
+    adj = synth(3000, 12000, seed=8)
+    G = pa.Graph.from_scipy(adj, device=DEV)
+    dZ = torch.randn(3000, 20, generator=torch.Generator().manual_seed(1)).bfloat16()
+    dH = to_np(pa.propagate_backward(G, dZ.to(DEV), 6, 0.1))
+    ref = O.appnp_backward(O.calc_a_hat(adj, "sym"), dZ.float().numpy(), 6, 0.1)
+    assert np.abs(dH - ref).max() <= 2e-2 * np.abs(ref).max()

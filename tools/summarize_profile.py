@@ -87,6 +87,13 @@ def main():
             line = line.strip()
             if line.startswith("{") and '"metric"' in line:
                 summ["bench"] = json.loads(line)
+    if "bench" in summ:
+        b = summ["bench"]
+        key = f"{b['config']['workload']}:{b['dtype']}:{b['config']['parallelism']}"
+        tpath = os.path.join(prof, "pmc_traffic.json")
+        table = json.load(open(tpath)) if os.path.exists(tpath) else {}
+        table[key] = fetch_b + write_b
+        json.dump(table, open(tpath, "w"), indent=1, sort_keys=True)
     out = os.path.join(prof, f"{a.tag}_summary.json")
     json.dump(summ, open(out, "w"), indent=1)
     print(json.dumps(summ["pmc"], indent=1))
