@@ -12,6 +12,8 @@
  *                                            launches  Z <- (1-a) A_hat Z + a H
  *   appnp_propagate_bwd   model.py:63        autograd of the same product (dH = J^T dZ)
  *   appnp_step            one iteration; used by the row-partitioned multi-GPU driver
+ *   appnp_standardize     ppnp/data/sparsegraph.py:191-222  SparseGraph.standardize
+ *                         (unweighted, undirected, no self loops, largest CC)
  *
  * Conventions
  *   - Every function returns 0 (APPNP_OK) or a negative errno-style code; nothing throws or
@@ -70,7 +72,25 @@ int appnp_graph_create(const int32_t* indptr, const int32_t* indices, const floa
                        int64_t n, int64_t nnz, int mode, void* stream, appnp_graph** out);
 
 /*
- * Same, but keeps only rows [row_lo, row_hi) of A_hat (global column indices); degrees of
+ * Device-side SparseGraph.standardize (ppnp/data/sparsegraph.py:191-222): unweighted,
+ * undirected (pattern of A + A^T), no self loops and, if select_lcc, only the largest
+ * connected component with nodes renumbered in increasing order (create_subgraph,
+ * sparsegraph.py:300-352).  Input: CSR of the raw adjacency (device; vals may be NULL;
+ * explicit zero weights count as absent).  Output: a handle owning the standardized int32
+ * CSR (sorted columns) and node_map[n_out] (int64 input node id of each kept node), which
+ * subsets attributes/labels exactly as the reference does.  Allocates and synchronises.
+ * Ties for the largest component go to the one with the largest smallest node index.
+ */
+typedef struct appnp_csr appnp_csr;
+int appnp_standardize(const int32_t* indptr, const int32_t* indices, const float* vals,
+                      int64_t n, int64_t nnz, int select_lcc, void* stream, appnp_csr** out);
+int appnp_csr_info(const appnp_csr* c, int64_t* n, int64_t* nnz, int64_t* n_in);
+int appnp_csr_copy(const appnp_csr* c, int32_t* indptr, int32_t* indices, int64_t* node_map,
+                   void* stream);
+void appnp_csr_destroy(appnp_csr* c);
+
+/*
+ * Same as appnp_graph_create, but keeps only rows [row_lo, row_hi) of A_hat (global column indices); degrees of
  * all n nodes are still computed from the full A.  Used for the row-partitioned multi-GPU
  * path: rank r owns rows [row_lo, row_hi).  With split_local != 0 the rows are also stored
  * as two CSRs -- columns inside [row_lo,row_hi) ("local") and outside ("remote") -- so the

@@ -55,6 +55,10 @@ _SIGS = {
         _i32,
         [_vp, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _f32, _f32, _u64, _vp, _sz, _vp],
     ),
+    "appnp_standardize": (_i32, [_vp, _vp, _vp, _i64, _i64, _i32, _vp, C.POINTER(_vp)]),
+    "appnp_csr_info": (_i32, [_vp, C.POINTER(_i64), C.POINTER(_i64), C.POINTER(_i64)]),
+    "appnp_csr_copy": (_i32, [_vp, _vp, _vp, _vp, _vp]),
+    "appnp_csr_destroy": (None, [_vp]),
     "appnp_step": (
         _i32,
         [_vp, _i32, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _f32,

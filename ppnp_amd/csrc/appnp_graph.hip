@@ -222,7 +222,14 @@ __global__ __launch_bounds__(kBlock) void k_scan_apply(const int32_t* __restrict
   if (blockIdx.x == 0 && threadIdx.x == 0) out[rows] = (int32_t)*grand;
 }
 
+}  // namespace
+
 // Scan cnt[rows] into out[rows+1]; the int64 total lands in *d_total (device).
+// d_bsum needs scan_partials(rows) int64 entries.
+int64_t scan_partials(int64_t rows) {
+  return std::max<int64_t>(1, (rows + kScanTile - 1) / kScanTile);
+}
+
 hipError_t exclusive_scan(const int32_t* cnt, int64_t rows, int32_t* out, int64_t* d_bsum,
                           int64_t* d_total, hipStream_t s) {
   const int64_t nb = std::max<int64_t>(1, (rows + kScanTile - 1) / kScanTile);
@@ -232,6 +239,8 @@ hipError_t exclusive_scan(const int32_t* cnt, int64_t rows, int32_t* out, int64_
                      d_total, out);
   return hipGetLastError();
 }
+
+namespace {
 
 template <typename T>
 hipError_t dalloc(T** p, int64_t count) {

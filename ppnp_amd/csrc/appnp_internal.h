@@ -35,6 +35,9 @@ int graph_build(const int32_t* indptr, const int32_t* indices, const float* vals
                 int64_t nnz, int mode, int64_t row_lo, int64_t row_hi, int split,
                 hipStream_t s, appnp_graph* g);
 void graph_free(appnp_graph* g);
+int64_t scan_partials(int64_t rows);
+hipError_t exclusive_scan(const int32_t* cnt, int64_t rows, int32_t* out, int64_t* d_bsum,
+                          int64_t* d_total, hipStream_t s);
 
 // appnp_spmm.hip
 int pick_vec(int dtype, int64_t f, const int64_t* lds, int n_ld, const void* const* ptrs,

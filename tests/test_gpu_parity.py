@@ -389,3 +389,61 @@ def test_bf16_backward():
     dH = to_np(pa.propagate_backward(G, dZ.to(DEV), 6, 0.1))
     ref = O.appnp_backward(O.calc_a_hat(adj, "sym"), dZ.float().numpy(), 6, 0.1)
     assert np.abs(dH - ref).max() <= 2e-2 * np.abs(ref).max()
+
+
+# ---------------------------------------------------------------------------------------
+# device SparseGraph.standardize (sparsegraph.py:191-222) vs the oracle / reference fixtures
+# ---------------------------------------------------------------------------------------
+
+
+def _std_check(adj, select_lcc=True):
+    from ppnp_amd.data import standardize_device
+
+    a = sp.csr_matrix(adj, dtype=np.float32)
+    a.sort_indices()
+    ip, ix, nm = standardize_device(a.indptr, a.indices, a.data, a.shape[0],
+                                    select_lcc=select_lcc, device=DEV)
+    ref, keep = O.standardize(a, select_lcc=select_lcc)
+    assert np.array_equal(nm.cpu().numpy(), keep)
+    assert np.array_equal(ip.cpu().numpy(), ref.indptr)
+    assert np.array_equal(ix.cpu().numpy(), ref.indices)
+
+
+@pytest.mark.parametrize("ds", ["cora", "citeseer"])
+def test_standardize_reference_datasets(ds, request):
+    g = request.getfixturevalue(ds)
+    n = int(g["adj_raw_n"])
+    raw = sp.csr_matrix((g["adj_raw_data"], g["adj_raw_indices"], g["adj_raw_indptr"]),
+                        shape=(n, n))
+    _std_check(raw)
+    # and it lands exactly on the reference's standardized adjacency
+    from ppnp_amd.data import standardize_device
+
+    ip, ix, _ = standardize_device(raw.indptr, raw.indices, raw.data, n, device=DEV)
+    assert np.array_equal(ip.cpu().numpy(), g["adj_indptr"])
+    assert np.array_equal(ix.cpu().numpy(), g["adj_indices"])
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_standardize_messy_graphs(seed):
+    rng = np.random.default_rng(seed)
+    n = 3000
+    # directed, weighted, self loops, many small components + duplicates
+    src = rng.integers(0, n, 4000)
+    dst = np.where(rng.random(4000) < 0.7, (src + rng.integers(1, 30, 4000)) % n,
+                   rng.integers(0, n, 4000))
+    w = rng.choice([1.0, 2.0, 0.5], 4000).astype(np.float32)
+    a = sp.coo_matrix((w, (src, dst)), shape=(n, n)).tocsr()
+    a.setdiag(np.where(rng.random(n) < 0.1, 3.0, 0.0))
+    a.eliminate_zeros()
+    _std_check(a, select_lcc=True)
+    _std_check(a, select_lcc=False)
+
+
+def test_standardize_tie_and_isolated():
+    # two components of equal size (ties -> the one with the larger smallest node), isolated
+    rows = [0, 1, 5, 6, 9]
+    cols = [1, 2, 6, 7, 9]
+    a = sp.csr_matrix((np.ones(5, np.float32), (rows, cols)), shape=(10, 10))
+    _std_check(a)
+    _std_check(sp.csr_matrix((10, 10), dtype=np.float32))
