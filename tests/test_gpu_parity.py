@@ -447,3 +447,63 @@ def test_standardize_tie_and_isolated():
     a = sp.csr_matrix((np.ones(5, np.float32), (rows, cols)), shape=(10, 10))
     _std_check(a)
     _std_check(sp.csr_matrix((10, 10), dtype=np.float32))
+
+
+# ---------------------------------------------------------------------------------------
+# batch-main.py's PPR rows (batch-main.py:111-117, 140-146) without the dense inverse
+# ---------------------------------------------------------------------------------------
+
+
+@pytest.mark.parametrize("mode", ["sym", "rw"])
+def test_ppr_rows_match_compute_ppr(cora, mode):
+    from ppnp_amd.ppr import ppr_rows
+
+    pa = _lib()
+    adj = adj_of(cora)
+    G = pa.Graph.from_scipy(adj, mode=mode, device=DEV)
+    idx = torch.tensor([0, 5, 17, 2809, 1400, 77])
+    rows = ppr_rows(G, idx, K=200, alpha=0.1).cpu().numpy()
+    ref = O.compute_ppr(adj, 0.1, mode)[idx.numpy()]
+    assert np.abs(rows - ref).max() <= 1e-5 * np.abs(ref).max()
+    top = ppr_rows(G, idx, K=200, alpha=0.1, topk=64).cpu().numpy()
+    assert ((top > 0).sum(1) >= 64).all() and ((top > 0).sum(1) <= 66).all()
+    for r in range(len(idx)):
+        ref_top = set(np.argsort(-ref[r])[:60])
+        assert ref_top <= set(np.nonzero(top[r])[0])
+
+
+def test_batch_topk_quirk_matches_batch_main(cora):
+    """batch-main.py:115-116 verbatim on the reference PPR vs the APPNP-built one."""
+    from ppnp_amd.ppr import batch_topk_quirk
+
+    pa = _lib()
+    adj = adj_of(cora)
+    G = pa.Graph.from_scipy(adj, device=DEV)
+    P = batch_topk_quirk(G, 128, K=200, alpha=0.1).cpu()
+    ref = torch.FloatTensor(O.compute_ppr(adj, alpha=0.1))
+    thresh, _ = ref.topk(128, axis=-1)
+    ref[ref < thresh[:, -1]] = 0
+    kept, kept_ref = P > 0, ref > 0
+    assert (kept != kept_ref).float().mean() < 1e-4  # only near-ties may flip
+    both = kept & kept_ref
+    assert (P[both] - ref[both]).abs().max() <= 1e-5 * ref.abs().max()
+
+
+def test_minibatch_forward_like_batch_main(cora):
+    """The batch-main.py:140-146 call pattern with sparse PPR rows from APPNP."""
+    from ppnp_amd.ppr import ppr_rows
+
+    pa = _lib()
+    adj = adj_of(cora)
+    n, C = int(cora["n"]), int(cora["n_classes"])
+    X = torch.from_numpy(cora["ppnp_X"]).to(DEV)
+    model = pa.APPNP(n_features=X.shape[1], n_classes=C, adj=adj, K=200).to(DEV).eval()
+    model.encoder[1].weight.data.copy_(torch.from_numpy(cora["ppnp_W1"]))
+    model.encoder[4].weight.data.copy_(torch.from_numpy(cora["ppnp_W2"]))
+    idx_batch = torch.from_numpy(cora["ppnp_idx"][:32]).to(DEV)
+    ppr_sub = ppr_rows(model.graph(), idx_batch, K=200, alpha=0.1)
+    sel = (ppr_sub > 0).any(dim=0)
+    with torch.no_grad():
+        out = model(X[sel], idx=None, ppr=ppr_sub[:, sel]).cpu().numpy()
+    ref = cora["ppnp_logits"][:32]
+    assert np.abs(out - ref).max() <= 1e-4 * np.abs(ref).max()
