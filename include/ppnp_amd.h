@@ -14,6 +14,8 @@
  *   appnp_step            one iteration; used by the row-partitioned multi-GPU driver
  *   appnp_standardize     ppnp/data/sparsegraph.py:191-222  SparseGraph.standardize
  *                         (unweighted, undirected, no self loops, largest CC)
+ *   appnp_spmm            model.py:36-38,47  Dropout + X @ W1 of the encoder on a CSR X
+ *                         (main.py:91 densifies X; 1.76 % dense on Cora-ML)
  *
  * Conventions
  *   - Every function returns 0 (APPNP_OK) or a negative errno-style code; nothing throws or
@@ -88,6 +90,26 @@ int appnp_csr_info(const appnp_csr* c, int64_t* n, int64_t* nnz, int64_t* n_in);
 int appnp_csr_copy(const appnp_csr* c, int32_t* indptr, int32_t* indices, int64_t* node_map,
                    void* stream);
 void appnp_csr_destroy(appnp_csr* c);
+
+/* Transpose of a CSR (rows x cols) as a canonical CSR (cols x rows, columns = input rows in
+ * increasing order), values carried when vals != NULL.  appnp_csr_info reports n = cols,
+ * n_in = rows; appnp_csr_copy gives indptr/indices (node_map unused); appnp_csr_values the
+ * values.  Allocates and synchronises. */
+int appnp_csr_transpose(const int32_t* indptr, const int32_t* indices, const float* vals,
+                        int64_t rows, int64_t cols, int64_t nnz, void* stream, appnp_csr** out);
+int appnp_csr_values(const appnp_csr* c, float* data, void* stream);
+
+/*
+ * General sparse x dense product on the same fused kernel family (fp32):
+ *   C[rows, f] = (M o A) B,   A: CSR rows x cols (vals NULL = all ones), B: cols x f (ld_b)
+ * with optional entry dropout M (keep iff 24-bit hash of (seed, 0, i, j) >= p * 2^24, kept
+ * entries scaled by 1/(1-p)); transposed_key != 0 keys entry (i, j) as (j, i), so the product
+ * with A^T (appnp_csr_transpose) replays the mask of A -- the backward of a dropout SpMM.
+ * Used for the sparse encoder input (model.py:36-38, 47 on a CSR X; main.py:91 densifies X).
+ */
+int appnp_spmm(const int32_t* indptr, const int32_t* indices, const float* vals, int64_t rows,
+               int64_t cols, const float* B, int64_t ld_b, float* C, int64_t ld_c, int64_t f,
+               float p_drop, uint64_t seed, int transposed_key, void* stream);
 
 /*
  * Same as appnp_graph_create, but keeps only rows [row_lo, row_hi) of A_hat (global column indices); degrees of

@@ -9,6 +9,7 @@ from . import _lib
 from .graph import Graph
 from .model import APPNP, PPNP, CustomLinear
 from .ops import propagate, propagate_backward, propagate_forward, step
+from .sparse import SparseFeatures, sparse_linear
 
 __all__ = [
     "APPNP",
@@ -19,5 +20,7 @@ __all__ = [
     "propagate_forward",
     "propagate_backward",
     "step",
+    "SparseFeatures",
+    "sparse_linear",
     "_lib",
 ]

@@ -59,6 +59,12 @@ _SIGS = {
     "appnp_csr_info": (_i32, [_vp, C.POINTER(_i64), C.POINTER(_i64), C.POINTER(_i64)]),
     "appnp_csr_copy": (_i32, [_vp, _vp, _vp, _vp, _vp]),
     "appnp_csr_destroy": (None, [_vp]),
+    "appnp_csr_transpose": (_i32, [_vp, _vp, _vp, _i64, _i64, _i64, _vp, C.POINTER(_vp)]),
+    "appnp_csr_values": (_i32, [_vp, _vp, _vp]),
+    "appnp_spmm": (
+        _i32,
+        [_vp, _vp, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _i64, _f32, _u64, _i32, _vp],
+    ),
     "appnp_step": (
         _i32,
         [_vp, _i32, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _f32,

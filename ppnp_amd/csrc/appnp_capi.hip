@@ -288,6 +288,34 @@ int appnp_propagate_bwd(const appnp_graph* g, const void* dZ, int64_t ld_dz, voi
   return APPNP_OK;
 }
 
+int appnp_spmm(const int32_t* indptr, const int32_t* indices, const float* vals, int64_t rows,
+               int64_t cols, const float* B, int64_t ld_b, float* Cm, int64_t ld_c, int64_t f,
+               float p_drop, uint64_t seed, int transposed_key, void* stream) {
+  if (rows < 0 || cols < 0 || f < 0 || f > INT32_MAX) return APPNP_EINVAL;
+  if (!(p_drop >= 0.0f && p_drop < 1.0f)) return APPNP_EINVAL;
+  if (rows == 0 || f == 0) return APPNP_OK;
+  if (!indptr || !Cm || ld_c < f || (cols > 0 && (!B || ld_b < f))) return APPNP_EINVAL;
+  StepArgs a{};
+  a.row_ptr = indptr;
+  a.col = indices;
+  a.val = vals;
+  a.zin = B;
+  a.ld_in = ld_b;
+  a.out = Cm;
+  a.ld_out = ld_c;
+  a.n_rows = rows;
+  a.row_lo = 0;
+  a.f = (int32_t)f;
+  a.scale = 1.0f;
+  a.alpha = 0.0f;
+  a.tkey = transposed_key ? 1 : 0;
+  set_drop(a, p_drop, seed, 0);
+  const int64_t lds[2] = {ld_b, ld_c};
+  const void* ptrs[2] = {B, Cm};
+  const int V = appnp::pick_vec(APPNP_F32, f, lds, 2, ptrs, 2);
+  return dev_err(appnp::launch_step(APPNP_F32, appnp::EPI_PARTIAL, V, a, as_stream(stream)));
+}
+
 int appnp_step(const appnp_graph* g, int part, const void* Zin, int64_t ld_in, const void* H,
                int64_t ld_h, void* Zout, int64_t ld_out, const float* partial,
                int64_t ld_partial, int64_t f, int dtype, int k, float alpha, float p_drop,

@@ -31,6 +31,7 @@ struct appnp_csr {
   int32_t* indptr = nullptr;
   int32_t* indices = nullptr;
   int64_t* node_map = nullptr;  // [n] input node id of each kept node (ascending)
+  float* data = nullptr;        // values (transpose of a weighted CSR only)
 };
 
 namespace appnp {
@@ -312,13 +313,96 @@ int standardize(const int32_t* indptr, const int32_t* indices, const float* vals
 #undef TRY
 }
 
+namespace {
+
+__global__ __launch_bounds__(kBlock) void k_emit_t(const int32_t* __restrict__ indptr,
+                                                   const int32_t* __restrict__ indices,
+                                                   int64_t rows, int64_t cols,
+                                                   uint64_t* __restrict__ keys, unsigned* err) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= rows) return;
+  for (int32_t p = indptr[i]; p < indptr[i + 1]; ++p) {
+    const int64_t j = indices[p];
+    if (j < 0 || j >= cols) atomicOr(err, 2u);
+    keys[p] = ((uint64_t)(uint32_t)j << 32) | (uint64_t)i;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_low_word(const uint64_t* __restrict__ keys, int64_t m,
+                                                     int32_t* __restrict__ out) {
+  const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (e < m) out[e] = (int32_t)(keys[e] & 0xffffffffu);
+}
+
+}  // namespace
+
+// Stable transpose: sort (col, row) keys, carrying the values; rows of the transpose list the
+// input rows in increasing order, so the result is canonical CSR.
+int csr_transpose(const int32_t* indptr, const int32_t* indices, const float* vals, int64_t rows,
+                  int64_t cols, int64_t nnz, hipStream_t s, appnp_csr* out) {
+#define TRY(x)                                                                              \
+  do {                                                                                      \
+    hipError_t e_ = (x);                                                                    \
+    if (e_ != hipSuccess)                                                                   \
+      return (e_ == hipErrorOutOfMemory || e_ == hipErrorMemoryAllocation) ? APPNP_ENOMEM   \
+                                                                           : APPNP_EDEVICE; \
+  } while (0)
+  Buffers b;
+  float* vtmp = nullptr;
+  unsigned h_err = 0;
+  out->n = cols;
+  out->n_in = rows;
+  out->nnz = nnz;
+  TRY(alloc(&b.flags, 2));
+  TRY(hipMemsetAsync(b.flags, 0, 2 * sizeof(unsigned), s));
+  TRY(alloc(&b.keys, nnz));
+  TRY(alloc(&b.keys_sorted, nnz));
+  if (rows > 0) {
+    hipLaunchKernelGGL(k_emit_t, dim3(grid_of(rows)), dim3(kBlock), 0, s, indptr, indices, rows,
+                       cols, b.keys, b.flags);
+    TRY(hipGetLastError());
+  }
+  TRY(alloc(&out->indptr, cols + 1));
+  TRY(alloc(&out->indices, nnz));
+  if (vals) TRY(alloc(&out->data, nnz));
+  if (nnz > 0) {
+    size_t tmp = 0;
+    if (vals) {
+      TRY(rocprim::radix_sort_pairs(nullptr, tmp, b.keys, b.keys_sorted, vals, out->data,
+                                    (size_t)nnz, 0u, 64u, s));
+    } else {
+      TRY(rocprim::radix_sort_keys(nullptr, tmp, b.keys, b.keys_sorted, (size_t)nnz, 0u, 64u, s));
+    }
+    TRY(alloc(reinterpret_cast<char**>(&b.tmp), (int64_t)tmp));
+    if (vals) {
+      TRY(rocprim::radix_sort_pairs(b.tmp, tmp, b.keys, b.keys_sorted, vals, out->data,
+                                    (size_t)nnz, 0u, 64u, s));
+    } else {
+      TRY(rocprim::radix_sort_keys(b.tmp, tmp, b.keys, b.keys_sorted, (size_t)nnz, 0u, 64u, s));
+    }
+    hipLaunchKernelGGL(k_low_word, dim3(grid_of(nnz)), dim3(kBlock), 0, s, b.keys_sorted, nnz,
+                       out->indices);
+    TRY(hipGetLastError());
+  }
+  hipLaunchKernelGGL(k_row_ptr, dim3(grid_of(cols + 1)), dim3(kBlock), 0, s, b.keys_sorted, nnz,
+                     cols, out->indptr);
+  TRY(hipGetLastError());
+  TRY(hipMemcpyAsync(&h_err, b.flags, sizeof(h_err), hipMemcpyDeviceToHost, s));
+  TRY(hipStreamSynchronize(s));
+  (void)vtmp;
+  return h_err ? APPNP_EINVAL : APPNP_OK;
+#undef TRY
+}
+
 void csr_free(appnp_csr* c) {
   if (!c) return;
   if (c->indptr) (void)hipFree(c->indptr);
   if (c->indices) (void)hipFree(c->indices);
   if (c->node_map) (void)hipFree(c->node_map);
+  if (c->data) (void)hipFree(c->data);
   c->indptr = c->indices = nullptr;
   c->node_map = nullptr;
+  c->data = nullptr;
 }
 
 }  // namespace appnp
@@ -365,6 +449,34 @@ int appnp_csr_copy(const appnp_csr* c, int32_t* indptr, int32_t* indices, int64_
   if (e == hipSuccess && node_map && c->n)
     e = hipMemcpyAsync(node_map, c->node_map, c->n * sizeof(int64_t), hipMemcpyDeviceToDevice, s);
   return e == hipSuccess ? APPNP_OK : APPNP_EDEVICE;
+}
+
+int appnp_csr_transpose(const int32_t* indptr, const int32_t* indices, const float* vals,
+                        int64_t rows, int64_t cols, int64_t nnz, void* stream, appnp_csr** out) {
+  if (!out) return APPNP_EINVAL;
+  *out = nullptr;
+  if (rows < 0 || cols < 0 || nnz < 0) return APPNP_EINVAL;
+  if (rows > INT32_MAX || cols > INT32_MAX || nnz > INT32_MAX) return APPNP_ERANGE;
+  if ((rows > 0 && !indptr) || (nnz > 0 && !indices)) return APPNP_EINVAL;
+  appnp_csr* c = new (std::nothrow) appnp_csr();
+  if (!c) return APPNP_ENOMEM;
+  const int rc = appnp::csr_transpose(indptr, indices, vals, rows, cols, nnz,
+                                      reinterpret_cast<hipStream_t>(stream), c);
+  if (rc != APPNP_OK) {
+    appnp::csr_free(c);
+    delete c;
+    return rc;
+  }
+  *out = c;
+  return APPNP_OK;
+}
+
+int appnp_csr_values(const appnp_csr* c, float* data, void* stream) {
+  if (!c || !data) return APPNP_EINVAL;
+  if (!c->data || c->nnz == 0) return c->data ? APPNP_OK : APPNP_EINVAL;
+  return hipMemcpyAsync(data, c->data, c->nnz * sizeof(float), hipMemcpyDeviceToDevice,
+                        reinterpret_cast<hipStream_t>(stream)) == hipSuccess ? APPNP_OK
+                                                                             : APPNP_EDEVICE;
 }
 
 void appnp_csr_destroy(appnp_csr* c) {

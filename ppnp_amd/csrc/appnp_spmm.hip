@@ -183,7 +183,7 @@ __global__ __launch_bounds__(kBlock) void k_step_wide(StepArgs a) {
       float w = 0.0f;
       if (lane < n) {
         c = a.col[cb + lane];
-        w = edge_weight(a.val[cb + lane], a.row_lo + row, c, a);
+        w = edge_weight(a.val ? a.val[cb + lane] : 1.0f, a.row_lo + row, c, a);
       }
       tile[lane] = make_int2(c, __float_as_int(w));
       __builtin_amdgcn_wave_barrier();
@@ -258,7 +258,7 @@ __global__ __launch_bounds__(kBlock) void k_step_narrow(StepArgs a) {
       for (int u = 0; u < U; ++u) {
         if (e + u < end) {
           c[u] = a.col[e + u];
-          w[u] = edge_weight(a.val[e + u], a.row_lo + row, c[u], a);
+          w[u] = edge_weight(a.val ? a.val[e + u] : 1.0f, a.row_lo + row, c[u], a);
         } else {
           c[u] = 0;
           w[u] = 0.0f;

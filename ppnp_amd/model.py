@@ -20,6 +20,7 @@ from torch import nn
 
 from .graph import Graph
 from .ops import propagate
+from .sparse import SparseFeatures, sparse_linear
 
 
 class CustomLinear(nn.Module):
@@ -60,6 +61,20 @@ def _encoder(n_features, n_classes, hidden_dim, drop_prob, bias):
     )
 
 
+def _encode(encoder, X, training):
+    """encoder(X) (model.py:46-52); a SparseFeatures X takes the sparse path: the input
+    Dropout + CustomLinear become one dropout-SpMM on the GPU (ppnp_amd/sparse.py)."""
+    if not isinstance(X, SparseFeatures):
+        return encoder(X)
+    lin = encoder[1]
+    p = encoder[0].p if training else 0.0
+    seed = int(torch.randint(0, 2**62, (1,)).item()) if p > 0 else 0
+    h = sparse_linear(X, lin.weight, p, seed)
+    if lin.bias is not None:
+        h = h + lin.bias
+    return encoder[4](encoder[3](encoder[2](h)))
+
+
 class PPNP(nn.Module):
     """model.py:41-67, unchanged semantics (dense ``ppr`` buffer)."""
 
@@ -74,9 +89,9 @@ class PPNP(nn.Module):
 
     def forward(self, X, idx=None, ppr=None):
         if idx is not None:
-            return self.ppr[idx] @ self.encoder(X)
+            return self.ppr[idx] @ _encode(self.encoder, X, self.training)
         elif ppr is not None:
-            return ppr @ self.encoder(X)
+            return ppr @ _encode(self.encoder, X, self.training)
         else:
             raise Exception()
 
@@ -135,9 +150,10 @@ class APPNP(nn.Module):
         return propagate(self.graph(), Hc, self.K, self.alpha, p, seed).to(H.dtype)
 
     def forward(self, X, idx=None, ppr=None):
+        """X: dense tensor (as the reference) or ppnp_amd.SparseFeatures (CSR on the GPU)."""
         if idx is not None:
-            return self.propagate(self.encoder(X))[idx]
+            return self.propagate(_encode(self.encoder, X, self.training))[idx]
         elif ppr is not None:
-            return ppr @ self.encoder(X)
+            return ppr @ _encode(self.encoder, X, self.training)
         else:
             raise Exception()

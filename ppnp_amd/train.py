@@ -150,7 +150,12 @@ def run_once(adj, attr, labels, args, device):
     idx_split_args = {"ntrain_per_class": args.ntrain_per_class, "nstopping": args.nstopping,
                       "nknown": args.nknown, "seed": gen_seeds()}
     X = normalize_attributes(attr)
-    X = torch.FloatTensor(np.asarray(X.todense())).to(device)
+    if args.sparse_x:  # keep X sparse on the GPU (main.py:91 densifies it)
+        from .sparse import SparseFeatures
+
+        X = SparseFeatures.from_scipy(X, device=device)
+    else:
+        X = torch.FloatTensor(np.asarray(X.todense())).to(device)
     y = torch.LongTensor(labels)
     idx_train, idx_stop, idx_valid = gen_splits(labels, idx_split_args, test=args.test)
     idx_train, idx_stop, idx_valid = map(torch.LongTensor, (idx_train, idx_stop, idx_valid))
@@ -225,6 +230,8 @@ def parse_args(argv=None):
     p.add_argument("--K", type=int, default=10)
     p.add_argument("--edge-drop", type=float, default=0.0)
     p.add_argument("--model", default="appnp", choices=["appnp", "ppnp"])
+    p.add_argument("--sparse-x", action="store_true",
+                   help="keep the attribute matrix as a CSR on the GPU (sparse encoder input)")
     p.add_argument("--test", action="store_true")
     p.add_argument("--verbose", action="store_true")
     args = p.parse_args(argv)

@@ -507,3 +507,82 @@ def test_minibatch_forward_like_batch_main(cora):
         out = model(X[sel], idx=None, ppr=ppr_sub[:, sel]).cpu().numpy()
     ref = cora["ppnp_logits"][:32]
     assert np.abs(out - ref).max() <= 1e-4 * np.abs(ref).max()
+
+
+# ---------------------------------------------------------------------------------------
+# sparse encoder input (model.py:36-38, 47 on a CSR X): appnp_spmm / appnp_csr_transpose
+# ---------------------------------------------------------------------------------------
+
+
+def _rand_csr(rows, cols, density, seed):
+    a = sp.random(rows, cols, density=density, format="csr", dtype=np.float32,
+                  random_state=np.random.RandomState(seed))
+    a.sort_indices()
+    return a
+
+
+@pytest.mark.parametrize("F", [1, 7, 64, 130])
+def test_spmm_matches_dense(F):
+    from ppnp_amd.sparse import spmm
+
+    A = _rand_csr(900, 700, 0.02, F)
+    B = torch.randn(700, F, generator=torch.Generator().manual_seed(F))
+    dev = lambda x: torch.from_numpy(x).to(DEV)  # noqa: E731
+    Cm = spmm(dev(A.indptr), dev(A.indices), dev(A.data), 900, 700, B.to(DEV))
+    close_fp32(to_np(Cm), A.astype(np.float64) @ B.double().numpy())
+
+
+def test_spmm_dropout_mask_and_transpose():
+    from ppnp_amd.sparse import SparseFeatures, spmm
+
+    A = _rand_csr(500, 300, 0.05, 1)
+    X = SparseFeatures.from_scipy(A, device=DEV)
+    ip, ix, dv = X.transpose()
+    At = A.T.tocsr()
+    At.sort_indices()
+    assert np.array_equal(ip.cpu().numpy(), At.indptr)
+    assert np.array_equal(ix.cpu().numpy(), At.indices)
+    assert np.array_equal(dv.cpu().numpy(), At.data)
+    # mask: oracle counter hash at k = 0, kept entries scaled by 1/(1-p)
+    B = torch.randn(300, 16, generator=torch.Generator().manual_seed(2))
+    Cm = spmm(X.indptr, X.indices, X.data, 500, 300, B.to(DEV), p_drop=0.5, seed=11)
+    M = O.masked_operator(A.astype(np.float64), 0, 0.5, 11)
+    close_fp32(to_np(Cm), M @ B.double().numpy())
+    # transposed product with the transposed key replays the same mask: (M o A)^T
+    G = torch.randn(500, 16, generator=torch.Generator().manual_seed(3))
+    D = spmm(ip, ix, dv, 300, 500, G.to(DEV), p_drop=0.5, seed=11, transposed_key=True)
+    close_fp32(to_np(D), M.T @ G.double().numpy())
+
+
+def test_sparse_linear_grad():
+    from ppnp_amd.sparse import SparseFeatures, sparse_linear
+
+    A = _rand_csr(400, 250, 0.04, 5)
+    X = SparseFeatures.from_scipy(A, device=DEV)
+    W = torch.randn(250, 32, device=DEV, requires_grad=True)
+    Y = sparse_linear(X, W, p_drop=0.3, seed=7)
+    G = torch.randn_like(Y)
+    (Y * G).sum().backward()
+    M = torch.from_numpy(O.masked_operator(A.astype(np.float64), 0, 0.3, 7).toarray()).float()
+    Wd = W.detach().cpu().requires_grad_(True)
+    Yd = M @ Wd
+    (Yd * G.cpu()).sum().backward()
+    assert torch.allclose(Y.cpu(), Yd, atol=1e-5, rtol=1e-5)
+    assert torch.allclose(W.grad.cpu(), Wd.grad, atol=1e-4, rtol=1e-5)
+
+
+def test_model_sparse_input_matches_dense(cora):
+    from ppnp_amd.sparse import SparseFeatures
+
+    pa = _lib()
+    adj = adj_of(cora)
+    Xd = torch.from_numpy(cora["ppnp_X"])
+    Xd[Xd < 0.9] = 0  # make it sparse
+    Xs = SparseFeatures.from_scipy(sp.csr_matrix(Xd.numpy()), device=DEV)
+    C = int(cora["n_classes"])
+    model = pa.APPNP(n_features=Xd.shape[1], n_classes=C, adj=adj, K=10).to(DEV).eval()
+    idx = torch.arange(0, 2810, 7, device=DEV)
+    with torch.no_grad():
+        a = model(Xd.to(DEV), idx)
+        b = model(Xs, idx)
+    assert torch.allclose(a, b, atol=1e-5, rtol=1e-4)

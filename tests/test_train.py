@@ -60,3 +60,10 @@ def test_citeseer_accuracy_matches_run_sh():
     re-run today gives 0.733 +- 0.014 (profiles/r1_train_accuracy.md)."""
     s = T.main(["--dataset", "citeseer", "--n-runs", "4", "--seed", "123"])
     assert 0.70 <= s["valid_acc_mean"] <= 0.79, s
+
+
+@pytest.mark.gpu
+def test_cora_accuracy_sparse_input():
+    """Same protocol with X kept as a CSR on the GPU (sparse encoder input)."""
+    s = T.main(["--dataset", "cora_ml", "--n-runs", "3", "--seed", "123", "--sparse-x"])
+    assert 0.81 <= s["valid_acc_mean"] <= 0.89, s
