@@ -54,6 +54,11 @@ enum appnp_status {
 /* helpers.py:61-66: 'sym' = D^-1/2 (A+I) D^-1/2, 'rw' = D^-1 (A+I) */
 enum appnp_norm { APPNP_NORM_SYM = 0, APPNP_NORM_RW = 1 };
 
+/* OR into `mode` of appnp_graph_create: also build A_hat^T (full graphs only) so that
+ * appnp_propagate_bwd works for 'rw' and for directed graphs.  Not needed (and not built)
+ * for 'sym' on an undirected graph, where A_hat^T == A_hat. */
+#define APPNP_GRAPH_TRANSPOSE 0x100
+
 /* storage type of H / Z (accumulation is always fp32) */
 enum appnp_dtype { APPNP_F32 = 0, APPNP_BF16 = 1 };
 
@@ -161,8 +166,8 @@ int appnp_propagate(const appnp_graph* g, const void* H, int64_t ld_h, void* Z, 
 
 /*
  * dH = J^T dZ for the map H -> Z of appnp_propagate with the same (K, alpha, p_drop, seed).
- * Uses A_hat^T; supported when the graph is symmetric (sym mode on an undirected graph),
- * APPNP_ENOTSUP otherwise.
+ * Uses A_hat^T: A_hat itself for 'sym' on an undirected graph, otherwise the transpose built
+ * at creation with APPNP_GRAPH_TRANSPOSE; APPNP_ENOTSUP if neither is available.
  */
 int appnp_propagate_bwd(const appnp_graph* g, const void* dZ, int64_t ld_dz, void* dH,
                         int64_t ld_dh, int64_t f, int dtype, int K, float alpha, float p_drop,

@@ -24,6 +24,7 @@ APPNP_ERANGE = -34
 APPNP_ENOTSUP = -95
 
 NORM = {"sym": 0, "rw": 1}
+GRAPH_TRANSPOSE = 0x100
 F32, BF16 = 0, 1
 PART_ALL, PART_LOCAL, PART_REMOTE = 0, 1, 2
 

@@ -100,15 +100,22 @@ int appnp_graph_create_rows(const int32_t* indptr, const int32_t* indices, const
   if (!out) return APPNP_EINVAL;
   *out = nullptr;
   if (n < 0 || nnz < 0 || n > INT32_MAX || nnz > INT32_MAX) return n > INT32_MAX || nnz > INT32_MAX ? APPNP_ERANGE : APPNP_EINVAL;
+  const bool want_t = (mode & APPNP_GRAPH_TRANSPOSE) != 0;
+  mode &= ~APPNP_GRAPH_TRANSPOSE;
   if (mode != APPNP_NORM_SYM && mode != APPNP_NORM_RW) return APPNP_EINVAL;
   if (row_lo < 0 || row_hi < row_lo || row_hi > n) return APPNP_EINVAL;
+  if (want_t && (row_lo != 0 || row_hi != n)) return APPNP_EINVAL;
   if (n > 0 && !indptr) return APPNP_EINVAL;
   if (nnz > 0 && !indices) return APPNP_EINVAL;
   appnp_graph* g = new (std::nothrow) appnp_graph();
   if (!g) return APPNP_ENOMEM;
-  const int rc = appnp::graph_build(indptr, indices, vals, n, nnz, mode, row_lo, row_hi,
-                                    split_local, as_stream(stream), g);
+  int rc = appnp::graph_build(indptr, indices, vals, n, nnz, mode, row_lo, row_hi,
+                              split_local, as_stream(stream), g);
+  // A_hat^T for the adjoint, unless A_hat is symmetric already ('sym' on undirected A)
+  if (rc == APPNP_OK && want_t && !(g->mode == APPNP_NORM_SYM && g->symmetric))
+    rc = appnp::graph_build_transpose(g, as_stream(stream));
   if (rc != APPNP_OK) {
+    appnp::graph_free(g);
     delete g;
     return rc;
   }
@@ -234,8 +241,10 @@ int appnp_propagate_bwd(const appnp_graph* g, const void* dZ, int64_t ld_dz, voi
   int rc = check_common(g, f, dtype, K, alpha, p_drop);
   if (rc) return rc;
   if (g->row_lo != 0 || g->row_hi != g->n) return APPNP_EINVAL;
-  // A_hat^T is only available as A_hat itself: symmetric 'sym' operator
-  if (!(g->mode == APPNP_NORM_SYM && g->symmetric)) return APPNP_ENOTSUP;
+  // A_hat^T: A_hat itself for 'sym' on an undirected graph, else the transposed CSR built at
+  // creation (APPNP_GRAPH_TRANSPOSE)
+  const bool self_adjoint = g->mode == APPNP_NORM_SYM && g->symmetric;
+  if (!self_adjoint && !g->t_row_ptr) return APPNP_ENOTSUP;
   const int64_t n = g->n;
   if (n == 0 || f == 0) return APPNP_OK;
   if (!dZ || !dH || ld_dz < f || ld_dh < f || dZ == dH) return APPNP_EINVAL;
@@ -265,7 +274,12 @@ int appnp_propagate_bwd(const appnp_graph* g, const void* dZ, int64_t ld_dz, voi
   rc = dev_err(appnp::launch_scale_rows(dtype, dZ, ld_dz, dH, ld_dh, n, f, alpha, s));
   if (rc) return rc;
   StepArgs a = base_args(g, f, alpha);
-  a.tkey = 1;
+  if (!self_adjoint) {
+    a.row_ptr = g->t_row_ptr;
+    a.col = g->t_col;
+    a.val = g->t_val;
+  }
+  a.tkey = 1;  // entry (j, i) of A_hat^T carries the mask of forward edge (i, j)
   a.aux = dH;
   a.ld_aux = ld_dh;
   const void* src = dZ;

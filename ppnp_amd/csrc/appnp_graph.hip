@@ -254,12 +254,14 @@ hipError_t dalloc(T** p, int64_t count) {
 void graph_free(appnp_graph* g) {
   if (!g) return;
   void* ptrs[] = {g->row_ptr, g->col, g->val, g->lrow_ptr, g->lcol, g->lval,
-                  g->rrow_ptr, g->rcol, g->rval, g->dinv};
+                  g->rrow_ptr, g->rcol, g->rval, g->dinv, g->t_row_ptr, g->t_col, g->t_val};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   g->row_ptr = g->col = g->lrow_ptr = g->lcol = g->rrow_ptr = g->rcol = nullptr;
   g->val = g->lval = g->rval = nullptr;
   g->dinv = nullptr;
+  g->t_row_ptr = g->t_col = nullptr;
+  g->t_val = nullptr;
 }
 
 #define APPNP_TRY(expr)                                                         \

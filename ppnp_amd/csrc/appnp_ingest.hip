@@ -394,6 +394,21 @@ int csr_transpose(const int32_t* indptr, const int32_t* indices, const float* va
 #undef TRY
 }
 
+// A_hat^T of a built graph, moved into the graph's t_* arrays.
+int graph_build_transpose(appnp_graph* g, hipStream_t s) {
+  appnp_csr t;
+  const int rc = csr_transpose(g->row_ptr, g->col, g->val, g->n, g->n, g->nnz_hat, s, &t);
+  if (rc != APPNP_OK) {
+    csr_free(&t);
+    return rc;
+  }
+  g->t_row_ptr = t.indptr;
+  g->t_col = t.indices;
+  g->t_val = t.data;
+  if (t.node_map) (void)hipFree(t.node_map);
+  return APPNP_OK;
+}
+
 void csr_free(appnp_csr* c) {
   if (!c) return;
   if (c->indptr) (void)hipFree(c->indptr);

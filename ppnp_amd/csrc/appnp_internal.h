@@ -26,7 +26,12 @@ struct appnp_graph {
   int32_t* rcol = nullptr;
   float* rval = nullptr;
   double* dinv = nullptr;       // [n] 1/sqrt(D) (sym) or 1/D (rw), fp64
+  int32_t* t_row_ptr = nullptr; // A_hat^T (APPNP_GRAPH_TRANSPOSE, when A_hat is not symmetric)
+  int32_t* t_col = nullptr;
+  float* t_val = nullptr;
 };
+
+struct appnp_csr;
 
 namespace appnp {
 
@@ -35,7 +40,13 @@ int graph_build(const int32_t* indptr, const int32_t* indices, const float* vals
                 int64_t nnz, int mode, int64_t row_lo, int64_t row_hi, int split,
                 hipStream_t s, appnp_graph* g);
 void graph_free(appnp_graph* g);
+int graph_build_transpose(appnp_graph* g, hipStream_t s);
 int64_t scan_partials(int64_t rows);
+
+// appnp_ingest.hip
+int csr_transpose(const int32_t* indptr, const int32_t* indices, const float* vals, int64_t rows,
+                  int64_t cols, int64_t nnz, hipStream_t s, appnp_csr* out);
+void csr_free(appnp_csr* c);
 hipError_t exclusive_scan(const int32_t* cnt, int64_t rows, int32_t* out, int64_t* d_bsum,
                           int64_t* d_total, hipStream_t s);
 

@@ -49,8 +49,10 @@ class Graph:
     # -- construction ---------------------------------------------------------------------
     @classmethod
     def from_csr(cls, indptr, indices, data, n, mode="sym", device=None, row_lo=0,
-                 row_hi=None, split_local=False):
-        """indptr/indices (int32) and optional data (fp32) of A; tensors or arrays."""
+                 row_hi=None, split_local=False, transpose=False):
+        """indptr/indices (int32) and optional data (fp32) of A; tensors or arrays.
+        ``transpose=True`` also builds A_hat^T when A_hat is not symmetric (rw mode or a
+        directed graph), which the backward needs."""
         if mode not in _lib.NORM:
             raise ValueError(f"mode must be 'sym' or 'rw', got {mode!r}")
         device = torch.device(device if device is not None else "cuda")
@@ -75,7 +77,8 @@ class Graph:
         out = C.c_void_p()
         with torch.cuda.device(device):
             rc = lib.appnp_graph_create_rows(
-                _ptr(ip), _ptr(ix), _ptr(dv), n, nnz, _lib.NORM[mode], int(row_lo), row_hi,
+                _ptr(ip), _ptr(ix), _ptr(dv), n, nnz,
+                _lib.NORM[mode] | (_lib.GRAPH_TRANSPOSE if transpose else 0), int(row_lo), row_hi,
                 1 if split_local else 0, C.c_void_p(_stream_ptr(device)), C.byref(out),
             )
         _lib.check("appnp_graph_create", rc)

@@ -137,7 +137,8 @@ class APPNP(nn.Module):
         dev = self.adj_indptr.device
         if self._graph is None or self._graph.device != dev:
             self._graph = Graph.from_csr(self.adj_indptr, self.adj_indices, self.adj_data,
-                                         self.n_nodes, mode=self.mode, device=dev)
+                                         self.n_nodes, mode=self.mode, device=dev,
+                                         transpose=True)
         return self._graph
 
     def get_norm(self):

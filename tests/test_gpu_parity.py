@@ -260,13 +260,30 @@ def test_autograd_gradcheck_small():
     assert abs(lhs - rhs) <= 1e-4 * max(1.0, abs(lhs))
 
 
-def test_backward_unsupported_for_rw():
+def test_backward_unsupported_without_transpose():
     pa = _lib()
     adj = synth(100, 300, seed=1)
     G = pa.Graph.from_scipy(adj, mode="rw", device=DEV)
     with pytest.raises(pa._lib.AppnpError) as e:
         pa.propagate_backward(G, torch.randn(100, 3, device=DEV), 3, 0.1)
     assert e.value.code == pa._lib.APPNP_ENOTSUP
+
+
+@pytest.mark.parametrize("mode", ["rw", "sym"])
+@pytest.mark.parametrize("directed", [False, True])
+@pytest.mark.parametrize("p", [0.0, 0.25])
+def test_backward_with_transpose(mode, directed, p):
+    """rw and directed graphs: the adjoint runs over A_hat^T built at creation."""
+    pa = _lib()
+    adj = synth(1200, 5000, seed=3)
+    if directed:
+        adj = sp.triu(adj, format="csr").astype(np.float32)
+        adj.sort_indices()
+    G = pa.Graph.from_scipy(adj, mode=mode, device=DEV, transpose=True)
+    dZ = torch.randn(1200, 6, generator=torch.Generator().manual_seed(2))
+    dH = to_np(pa.propagate_backward(G, dZ.to(DEV), 5, 0.1, p_drop=p, seed=8))
+    ref = O.appnp_backward(O.calc_a_hat(adj, mode), dZ.numpy(), 5, 0.1, p_drop=p, seed=8)
+    close_fp32(dH, ref)
 
 
 # ---------------------------------------------------------------------------------------
