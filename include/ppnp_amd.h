@@ -86,7 +86,9 @@ int appnp_graph_create(const int32_t* indptr, const int32_t* indices, const floa
  * explicit zero weights count as absent).  Output: a handle owning the standardized int32
  * CSR (sorted columns) and node_map[n_out] (int64 input node id of each kept node), which
  * subsets attributes/labels exactly as the reference does.  Allocates and synchronises.
- * Ties for the largest component go to the one with the largest smallest node index.
+ * Ties for the largest component go to the one with the largest smallest node index (the
+ * reference's np.argsort(sizes)[::-1][:1] is not stable, so its own tie order depends on the
+ * numpy build; real datasets have a unique largest component).
  */
 typedef struct appnp_csr appnp_csr;
 int appnp_standardize(const int32_t* indptr, const int32_t* indices, const float* vals,

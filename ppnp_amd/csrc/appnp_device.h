@@ -29,6 +29,7 @@ struct StepArgs {
   void* aux;               // BWD: dH (storage dtype); FINISH: fp32 partial
   int64_t ld_in, ld_h, ld_out, ld_aux;
   int64_t n_rows;          // rows held
+  int64_t zin_rows;        // rows of zin (its last row is never over-read)
   int64_t row_lo;          // global index of local row 0 (hash key only)
   uint64_t mkey;           // per-iteration dropout key = splitmix64(seed + (k+1)*golden)
   int32_t f;               // features

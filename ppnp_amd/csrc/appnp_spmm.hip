@@ -29,10 +29,13 @@ namespace appnp {
 namespace {
 
 // ---- row fragments: V consecutive elements at p.  With TAIL, a lane whose fragment crosses
-// the end of the row (rem = f - col0 < V valid elements) reads/writes exactly those rem
-// elements, in descending power-of-two pieces at compile-time offsets (no over-read past F,
-// no runtime register indexing).  All tail lanes of a wave share rem, so the switch is
-// wave-uniform.
+// the end of the row (rem = f - col0 < V valid elements) WRITES exactly those rem elements,
+// in descending power-of-two pieces at compile-time offsets (no runtime register indexing).
+// It READS a full vector whenever that stays inside the buffer -- every row but the buffer's
+// last, since ld >= roundup(F, V) puts the over-read inside the next row -- so a gather stays
+// one load instruction (one set of line requests); only the last row is read piecewise.
+// Padding values read that way land in accumulator slots that are never stored.  All tail
+// lanes of a wave share rem, so the switches are wave-uniform.
 template <typename T, int N, int O, int V>
 __device__ __forceinline__ void ld_at(const T* p, float (&x)[V]) {
   float t[N];
@@ -50,8 +53,8 @@ __device__ __forceinline__ void st_at(T* p, const float (&x)[V]) {
 }
 
 template <typename T, int V, bool TAIL>
-__device__ __forceinline__ void frag_load(const T* p, float (&x)[V], int rem) {
-  if (!TAIL || rem >= V) {
+__device__ __forceinline__ void frag_load(const T* p, float (&x)[V], int rem, bool full_ok) {
+  if (!TAIL || rem >= V || full_ok) {
     Io<T, V>::load(p, x);
     return;
   }
@@ -124,7 +127,7 @@ __device__ __forceinline__ void epilogue(const StepArgs& a, int64_t row, int col
     if (a.out) frag_store<T, V, TAIL>(static_cast<T*>(a.out) + row * a.ld_out + col0, y, rem);
     T* d = static_cast<T*>(a.aux) + row * a.ld_aux + col0;
     float dv[V];
-    frag_load<T, V, TAIL>(d, dv, rem);
+    frag_load<T, V, TAIL>(d, dv, rem, row + 1 < a.n_rows);
 #pragma unroll
     for (int v = 0; v < V; ++v) dv[v] = fmaf(a.alpha, y[v], dv[v]);
     frag_store<T, V, TAIL>(d, dv, rem);
@@ -132,7 +135,8 @@ __device__ __forceinline__ void epilogue(const StepArgs& a, int64_t row, int col
     frag_store<float, V, TAIL>(static_cast<float*>(a.out) + row * a.ld_out + col0, y, rem);
   } else {  // EPI_FINISH
     float pv[V];
-    frag_load<float, V, TAIL>(static_cast<const float*>(a.aux) + row * a.ld_aux + col0, pv, rem);
+    frag_load<float, V, TAIL>(static_cast<const float*>(a.aux) + row * a.ld_aux + col0, pv, rem,
+                              row + 1 < a.n_rows);
 #pragma unroll
     for (int v = 0; v < V; ++v) y[v] = fmaf(a.alpha, hv[v], y[v] + pv[v]);
     frag_store<T, V, TAIL>(static_cast<T*>(a.out) + row * a.ld_out + col0, y, rem);
@@ -143,7 +147,8 @@ template <typename T, int V, int EPI, bool TAIL>
 __device__ __forceinline__ void load_h(const StepArgs& a, int64_t row, int col0, float (&hv)[V],
                                        int rem) {
   if constexpr (EPI == EPI_FWD || EPI == EPI_FINISH) {
-    frag_load<T, V, TAIL>(static_cast<const T*>(a.h) + row * a.ld_h + col0, hv, rem);
+    frag_load<T, V, TAIL>(static_cast<const T*>(a.h) + row * a.ld_h + col0, hv, rem,
+                          row + 1 < a.n_rows);
   } else {
 #pragma unroll
     for (int v = 0; v < V; ++v) hv[v] = 0.0f;
@@ -198,7 +203,8 @@ __global__ __launch_bounds__(kBlock) void k_step_wide(StepArgs a) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           if (fact && t + u * P < n) {
-            frag_load<T, V, TAIL>(zin + (int64_t)e[u].x * a.ld_in + col0, z[u], rem);
+            frag_load<T, V, TAIL>(zin + (int64_t)e[u].x * a.ld_in + col0, z[u], rem,
+                                  e[u].x + 1 < a.zin_rows);
           } else {
 #pragma unroll
             for (int v = 0; v < V; ++v) z[u][v] = 0.0f;
@@ -267,7 +273,8 @@ __global__ __launch_bounds__(kBlock) void k_step_narrow(StepArgs a) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if (fact && e + u < end) {
-          frag_load<T, V, TAIL>(zin + (int64_t)c[u] * a.ld_in + col0, z[u], rem);
+          frag_load<T, V, TAIL>(zin + (int64_t)c[u] * a.ld_in + col0, z[u], rem,
+                                c[u] + 1 < a.zin_rows);
         } else {
 #pragma unroll
           for (int v = 0; v < V; ++v) z[u][v] = 0.0f;

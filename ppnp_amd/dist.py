@@ -73,15 +73,26 @@ def col_range(f: int, C: int, ci: int):
     return lo, lo + base + (1 if ci < rem else 0)
 
 
+def _avg_lines(row_bytes: int, stride: int) -> float:
+    """Average number of 128-B lines a row of ``row_bytes`` spans at row stride ``stride``."""
+    period = 128 // math.gcd(128, stride % 128 or 128)
+    return sum(((i * stride) % 128 + row_bytes - 1) // 128 + 1 for i in range(period)) / period
+
+
 def line_ld(width: int, elem_bytes: int = 4) -> int:
-    """Leading dimension (elements) that keeps a row inside as few 128-B lines as possible:
-    the next power of two up to a line, then a multiple of the line."""
+    """Leading dimension (elements) for row gathers: rows padded to start on a 128-B line (next
+    power of two up to a line, then whole lines) when that lowers the average lines a row
+    spans; otherwise packed to a 16-B multiple.  Same rule as appnp_capi.hip line_ld."""
     if width <= 0:
         return 1
     line = 128 // elem_bytes
-    if width <= line:
-        return 1 << (width - 1).bit_length()
-    return -(-width // line) * line
+    padded = (1 << (width - 1).bit_length()) if width <= line else -(-width // line) * line
+    v = 16 // elem_bytes
+    packed = -(-width // v) * v
+    if _avg_lines(width * elem_bytes, padded * elem_bytes) < _avg_lines(width * elem_bytes,
+                                                                        packed * elem_bytes):
+        return padded
+    return packed
 
 
 class _TorchComm:

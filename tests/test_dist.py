@@ -113,6 +113,7 @@ def test_layout_helpers():
     cols = [col_range(100, 8, c) for c in range(8)]
     assert cols[0][0] == 0 and cols[-1][1] == 100
     assert all(b - a in (12, 13) for a, b in cols)
-    assert line_ld(25) == 32 and line_ld(13) == 16 and line_ld(50) == 64 and line_ld(100) == 128
-    assert line_ld(7) == 8 and line_ld(40, 2) == 64
+    # padded only where it lowers the lines per row: 100 fp32 (400 B) spans 4 lines either way
+    assert line_ld(25) == 32 and line_ld(13) == 16 and line_ld(50) == 64 and line_ld(100) == 100
+    assert line_ld(7) == 8 and line_ld(40, 2) == 64 and line_ld(100, 2) == 128
     assert choose_layout(8, 2_449_029, 100, 126_000_000) == Layout(1, 8)
