@@ -95,6 +95,9 @@ StepArgs base_args(const appnp_graph* g, int64_t f, float alpha) {
   a.scale = 1.0f - alpha;
   a.alpha = alpha;
   a.drop_scale = 1.0f;
+  a.heavy = g->heavy;
+  a.n_heavy = g->n_heavy;
+  a.heavy_thr = appnp::kHeavyRow;
   return a;
 }
 
@@ -300,6 +303,8 @@ int appnp_propagate_bwd(const appnp_graph* g, const void* dZ, int64_t ld_dz, voi
     a.row_ptr = g->t_row_ptr;
     a.col = g->t_col;
     a.val = g->t_val;
+    a.heavy = g->t_heavy;
+    a.n_heavy = g->t_n_heavy;
   }
   a.tkey = 1;  // entry (j, i) of A_hat^T carries the mask of forward edge (i, j)
   a.aux = dH;
@@ -381,6 +386,8 @@ int appnp_step(const appnp_graph* g, int part, const void* Zin, int64_t ld_in, c
   } else {
     if (!g->split) return APPNP_EINVAL;
     if (dtype != APPNP_F32) return APPNP_ENOTSUP;
+    a.heavy = nullptr;  // the heavy-row list describes the full rows, not their halves
+    a.n_heavy = 0;
     if (part == APPNP_PART_LOCAL) {
       epi = appnp::EPI_PARTIAL;
       a.row_ptr = g->lrow_ptr;

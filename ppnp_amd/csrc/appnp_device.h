@@ -38,7 +38,13 @@ struct StepArgs {
   float alpha;             // weight of H (FWD/FINISH) or of y into aux (BWD)
   float drop_scale;        // 1 / (1 - p)
   int32_t tkey;            // 1: hash key of entry (row i, col j) is (j, i)  (transposed operator)
+  const int32_t* heavy;    // rows longer than heavy_thr (narrow kernels give them a wave)
+  int64_t n_heavy;
+  int32_t heavy_thr;
+  int64_t light_blocks;    // set by launch_step: blocks [light_blocks, grid) take heavy rows
 };
+
+constexpr int kHeavyRow = 32;  // a row longer than this gets a whole wavefront
 
 __host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
   x += 0x9E3779B97F4A7C15ull;

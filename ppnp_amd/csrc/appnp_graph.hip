@@ -251,10 +251,67 @@ hipError_t dalloc(T** p, int64_t count) {
 
 }  // namespace
 
+namespace {
+
+__global__ __launch_bounds__(kBlock) void k_heavy_flags(const int32_t* __restrict__ rp, int64_t rows,
+                                                        int32_t thr, int32_t* __restrict__ flag) {
+  const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (r < rows) flag[r] = (rp[r + 1] - rp[r]) > thr ? 1 : 0;
+}
+
+__global__ __launch_bounds__(kBlock) void k_heavy_scatter(const int32_t* __restrict__ flag,
+                                                          const int32_t* __restrict__ pos,
+                                                          int64_t rows, int32_t* __restrict__ out) {
+  const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (r < rows && flag[r]) out[pos[r]] = (int32_t)r;
+}
+
+}  // namespace
+
+// Ascending list of the rows with more than kHeavyRow entries (load balance of the narrow
+// kernels on power-law graphs).  Synchronises (setup only).
+int build_heavy(const int32_t* rp, int64_t rows, hipStream_t s, int32_t** out, int64_t* n_out) {
+  *out = nullptr;
+  *n_out = 0;
+  if (rows <= 0) return APPNP_OK;
+  int32_t *flag = nullptr, *pos = nullptr;
+  int64_t *bsum = nullptr, *tot = nullptr;
+  int64_t h_tot = 0;
+  int rc = APPNP_OK;
+  const unsigned grid = (unsigned)((rows + kBlock - 1) / kBlock);
+  if (hipMalloc(&flag, rows * sizeof(int32_t)) != hipSuccess ||
+      hipMalloc(&pos, (rows + 1) * sizeof(int32_t)) != hipSuccess ||
+      hipMalloc(&bsum, scan_partials(rows) * sizeof(int64_t)) != hipSuccess ||
+      hipMalloc(&tot, sizeof(int64_t)) != hipSuccess) {
+    rc = APPNP_ENOMEM;
+  } else {
+    hipLaunchKernelGGL(k_heavy_flags, dim3(grid), dim3(kBlock), 0, s, rp, rows, kHeavyRow, flag);
+    if (exclusive_scan(flag, rows, pos, bsum, tot, s) != hipSuccess ||
+        hipMemcpyAsync(&h_tot, tot, sizeof(int64_t), hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess) {
+      rc = APPNP_EDEVICE;
+    } else if (h_tot > 0) {
+      if (hipMalloc(out, h_tot * sizeof(int32_t)) != hipSuccess) {
+        rc = APPNP_ENOMEM;
+      } else {
+        hipLaunchKernelGGL(k_heavy_scatter, dim3(grid), dim3(kBlock), 0, s, flag, pos, rows, *out);
+        if (hipStreamSynchronize(s) != hipSuccess) rc = APPNP_EDEVICE;
+        *n_out = h_tot;
+      }
+    }
+  }
+  if (flag) (void)hipFree(flag);
+  if (pos) (void)hipFree(pos);
+  if (bsum) (void)hipFree(bsum);
+  if (tot) (void)hipFree(tot);
+  return rc;
+}
+
 void graph_free(appnp_graph* g) {
   if (!g) return;
   void* ptrs[] = {g->row_ptr, g->col, g->val, g->lrow_ptr, g->lcol, g->lval,
-                  g->rrow_ptr, g->rcol, g->rval, g->dinv, g->t_row_ptr, g->t_col, g->t_val};
+                  g->rrow_ptr, g->rcol, g->rval, g->dinv, g->t_row_ptr, g->t_col, g->t_val,
+                  g->heavy, g->t_heavy};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   g->row_ptr = g->col = g->lrow_ptr = g->lcol = g->rrow_ptr = g->rcol = nullptr;
@@ -262,6 +319,7 @@ void graph_free(appnp_graph* g) {
   g->dinv = nullptr;
   g->t_row_ptr = g->t_col = nullptr;
   g->t_val = nullptr;
+  g->heavy = g->t_heavy = nullptr;
 }
 
 #define APPNP_TRY(expr)                                                         \
@@ -361,6 +419,7 @@ int graph_build(const int32_t* indptr, const int32_t* indices, const float* vals
   }
   APPNP_TRY(hipStreamSynchronize(s));
   (void)nnz;
+  rc = build_heavy(g->row_ptr, rows, s, &g->heavy, &g->n_heavy);
 
 done:
   if (cnt) (void)hipFree(cnt);

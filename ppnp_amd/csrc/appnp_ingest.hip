@@ -406,7 +406,7 @@ int graph_build_transpose(appnp_graph* g, hipStream_t s) {
   g->t_col = t.indices;
   g->t_val = t.data;
   if (t.node_map) (void)hipFree(t.node_map);
-  return APPNP_OK;
+  return build_heavy(g->t_row_ptr, g->n, s, &g->t_heavy, &g->t_n_heavy);
 }
 
 void csr_free(appnp_csr* c) {

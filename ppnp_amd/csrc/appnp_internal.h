@@ -26,6 +26,10 @@ struct appnp_graph {
   int32_t* rcol = nullptr;
   float* rval = nullptr;
   double* dinv = nullptr;       // [n] 1/sqrt(D) (sym) or 1/D (rw), fp64
+  int32_t* heavy = nullptr;     // rows with > kHeavyRow entries (ascending)
+  int64_t n_heavy = 0;
+  int32_t* t_heavy = nullptr;   // the same for A_hat^T
+  int64_t t_n_heavy = 0;
   int32_t* t_row_ptr = nullptr; // A_hat^T (APPNP_GRAPH_TRANSPOSE, when A_hat is not symmetric)
   int32_t* t_col = nullptr;
   float* t_val = nullptr;
@@ -41,6 +45,7 @@ int graph_build(const int32_t* indptr, const int32_t* indices, const float* vals
                 hipStream_t s, appnp_graph* g);
 void graph_free(appnp_graph* g);
 int graph_build_transpose(appnp_graph* g, hipStream_t s);
+int build_heavy(const int32_t* rp, int64_t rows, hipStream_t s, int32_t** out, int64_t* n_out);
 int64_t scan_partials(int64_t rows);
 
 // appnp_ingest.hip

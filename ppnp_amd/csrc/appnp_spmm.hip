@@ -156,10 +156,92 @@ __device__ __forceinline__ void load_h(const StepArgs& a, int64_t row, int col0,
 }
 
 // ------------------------------------------------------------------------------------------
-// wide: one wavefront per row, P = 64/G sub-groups split the row's entries
+// one wavefront on one row: P = 64/G sub-groups split the row's entries
+// ------------------------------------------------------------------------------------------
+template <typename T, int V, int G, int EPI, int U, bool TAIL>
+__device__ __forceinline__ void wave_row(const StepArgs& a, int64_t row, int lane, int2* tile,
+                                         int col0, int rem) {
+  constexpr int P = kWave / G;
+  const int sub = lane / G;
+  const bool fact = rem > 0;
+  const T* __restrict__ zin = static_cast<const T*>(a.zin);
+  const int beg = a.row_ptr[row];
+  const int end = a.row_ptr[row + 1];
+  float hv[V];
+  if (sub == 0 && fact) load_h<T, V, EPI, TAIL>(a, row, col0, hv, rem);
+  float acc[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) acc[v] = 0.0f;
+
+  for (int cb = beg; cb < end; cb += kWave) {
+    const int n = min(kWave, end - cb);
+    int c = 0;
+    float w = 0.0f;
+    if (lane < n) {
+      c = a.col[cb + lane];
+      w = edge_weight(a.val ? a.val[cb + lane] : 1.0f, a.row_lo + row, c, a);
+    }
+    tile[lane] = make_int2(c, __float_as_int(w));
+    __builtin_amdgcn_wave_barrier();
+    for (int t = sub; t < n; t += P * U) {
+      int2 e[U];
+      float z[U][V];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int idx = t + u * P;
+        e[u] = idx < n ? tile[idx] : make_int2(0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (fact && t + u * P < n) {
+          frag_load<T, V, TAIL>(zin + (int64_t)e[u].x * a.ld_in + col0, z[u], rem,
+                                e[u].x + 1 < a.zin_rows);
+        } else {
+#pragma unroll
+          for (int v = 0; v < V; ++v) z[u][v] = 0.0f;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const float wu = __int_as_float(e[u].y);
+#pragma unroll
+        for (int v = 0; v < V; ++v) acc[v] = fmaf(wu, z[u][v], acc[v]);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  // combine the P sub-group partial sums (butterfly, fixed order)
+#pragma unroll
+  for (int off = G; off < kWave; off <<= 1) {
+#pragma unroll
+    for (int v = 0; v < V; ++v) acc[v] += __shfl_xor(acc[v], off);
+  }
+  if (sub == 0 && fact) epilogue<T, V, EPI, TAIL>(a, row, col0, acc, hv, rem);
+}
+
+// ------------------------------------------------------------------------------------------
+// wide: one wavefront per row
 // ------------------------------------------------------------------------------------------
 template <typename T, int V, int G, int EPI, int U, bool TAIL>
 __global__ __launch_bounds__(kBlock) void k_step_wide(StepArgs a) {
+  __shared__ int2 stage[kWavesPerBlock][kWave];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int col0 = blockIdx.y * (G * V) + (lane % G) * V;
+  const int rem = a.f - col0;  // valid features of this lane's fragment (>= V: full)
+  const int64_t nwaves = (int64_t)gridDim.x * kWavesPerBlock;
+  for (int64_t row = (int64_t)blockIdx.x * kWavesPerBlock + wave; row < a.n_rows; row += nwaves)
+    wave_row<T, V, G, EPI, U, TAIL>(a, row, lane, stage[wave], col0, rem);
+}
+
+// ------------------------------------------------------------------------------------------
+// narrow: one G-lane group per row, P = 64/G rows per wave.  Rows longer than a.heavy_thr
+// (listed in a.heavy at graph creation) are skipped here and processed by the trailing
+// blocks (blockIdx.x >= a.light_blocks), one whole wavefront per row (wave_row), so a hub row
+// of a power-law graph does not serialise on G lanes while the rest of the launch waits.
+// ------------------------------------------------------------------------------------------
+template <typename T, int V, int G, int EPI, int U, bool TAIL>
+__global__ __launch_bounds__(kBlock) void k_step_narrow(StepArgs a) {
   constexpr int P = kWave / G;
   __shared__ int2 stage[kWavesPerBlock][kWave];
   const int lane = threadIdx.x & (kWave - 1);
@@ -170,87 +252,22 @@ __global__ __launch_bounds__(kBlock) void k_step_wide(StepArgs a) {
   const int rem = a.f - col0;  // valid features of this lane's fragment (>= V: full)
   const bool fact = rem > 0;
   const T* __restrict__ zin = static_cast<const T*>(a.zin);
-  int2* tile = stage[wave];
-  const int64_t nwaves = (int64_t)gridDim.x * kWavesPerBlock;
 
-  for (int64_t row = (int64_t)blockIdx.x * kWavesPerBlock + wave; row < a.n_rows; row += nwaves) {
-    const int beg = a.row_ptr[row];
-    const int end = a.row_ptr[row + 1];
-    float hv[V];
-    if (sub == 0 && fact) load_h<T, V, EPI, TAIL>(a, row, col0, hv, rem);
-    float acc[V];
-#pragma unroll
-    for (int v = 0; v < V; ++v) acc[v] = 0.0f;
-
-    for (int cb = beg; cb < end; cb += kWave) {
-      const int n = min(kWave, end - cb);
-      int c = 0;
-      float w = 0.0f;
-      if (lane < n) {
-        c = a.col[cb + lane];
-        w = edge_weight(a.val ? a.val[cb + lane] : 1.0f, a.row_lo + row, c, a);
-      }
-      tile[lane] = make_int2(c, __float_as_int(w));
-      __builtin_amdgcn_wave_barrier();
-      for (int t = sub; t < n; t += P * U) {
-        int2 e[U];
-        float z[U][V];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int idx = t + u * P;
-          e[u] = idx < n ? tile[idx] : make_int2(0, 0);
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          if (fact && t + u * P < n) {
-            frag_load<T, V, TAIL>(zin + (int64_t)e[u].x * a.ld_in + col0, z[u], rem,
-                                  e[u].x + 1 < a.zin_rows);
-          } else {
-#pragma unroll
-            for (int v = 0; v < V; ++v) z[u][v] = 0.0f;
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const float wu = __int_as_float(e[u].y);
-#pragma unroll
-          for (int v = 0; v < V; ++v) acc[v] = fmaf(wu, z[u][v], acc[v]);
-        }
-      }
-      __builtin_amdgcn_wave_barrier();
-    }
-    // combine the P sub-group partial sums (butterfly, fixed order)
-#pragma unroll
-    for (int off = G; off < kWave; off <<= 1) {
-#pragma unroll
-      for (int v = 0; v < V; ++v) acc[v] += __shfl_xor(acc[v], off);
-    }
-    if (sub == 0 && fact) epilogue<T, V, EPI, TAIL>(a, row, col0, acc, hv, rem);
+  if ((int64_t)blockIdx.x >= a.light_blocks) {  // heavy rows: a wavefront each
+    const int64_t hw = ((int64_t)blockIdx.x - a.light_blocks) * kWavesPerBlock + wave;
+    const int64_t hstride = ((int64_t)gridDim.x - a.light_blocks) * kWavesPerBlock;
+    for (int64_t h = hw; h < a.n_heavy; h += hstride)
+      wave_row<T, V, G, EPI, U, TAIL>(a, a.heavy[h], lane, stage[wave], col0, rem);
+    return;
   }
-}
-
-// ------------------------------------------------------------------------------------------
-// narrow: one G-lane group per row, P = 64/G rows per wave
-// ------------------------------------------------------------------------------------------
-template <typename T, int V, int G, int EPI, int U, bool TAIL>
-__global__ __launch_bounds__(kBlock) void k_step_narrow(StepArgs a) {
-  constexpr int P = kWave / G;
-  const int lane = threadIdx.x & (kWave - 1);
-  const int wave = threadIdx.x >> 6;
-  const int sub = lane / G;
-  const int gl = lane % G;
-  const int col0 = blockIdx.y * (G * V) + gl * V;
-  const int rem = a.f - col0;  // valid features of this lane's fragment (>= V: full)
-  const bool fact = rem > 0;
-  const T* __restrict__ zin = static_cast<const T*>(a.zin);
-  const int64_t stride = (int64_t)gridDim.x * kWavesPerBlock * P;
-
+  const int64_t stride = a.light_blocks * kWavesPerBlock * P;
   for (int64_t rb = ((int64_t)blockIdx.x * kWavesPerBlock + wave) * P; rb < a.n_rows;
        rb += stride) {
     const int64_t row = rb + sub;
     if (row >= a.n_rows) continue;
     const int beg = a.row_ptr[row];
     const int end = a.row_ptr[row + 1];
+    if (a.heavy && end - beg > a.heavy_thr) continue;
     float hv[V];
     if (fact) load_h<T, V, EPI, TAIL>(a, row, col0, hv, rem);
     float acc[V];
@@ -351,18 +368,39 @@ static int env_int(const char* name, int dflt) {
   return (s && *s) ? atoi(s) : dflt;
 }
 
-hipError_t launch_step(int dtype, int epi, int V, const StepArgs& a, hipStream_t s) {
+hipError_t launch_step(int dtype, int epi, int V, const StepArgs& a_in, hipStream_t s) {
+  StepArgs a = a_in;
   if (a.n_rows <= 0 || a.f <= 0) return hipSuccess;
   // lanes per row slab: smallest power of two covering min(F, 64V) features
-  const int64_t lanes_needed = (std::min<int64_t>(a.f, 64LL * V) + V - 1) / V;
-  int G = 1;
-  while (G < lanes_needed) G <<= 1;
+  auto lanes_for = [&](int v) {
+    const int64_t need = (std::min<int64_t>(a.f, 64LL * v) + v - 1) / v;
+    int g = 1;
+    while (g < need) g <<= 1;
+    return g;
+  };
+  // Small graphs are latency-bound: keep >= kMinWaves wavefronts in flight by narrowing the
+  // vector (more lanes per row, fewer rows per wave) before settling on V.
+  constexpr int64_t kMinWaves = 2048;
+  int G = lanes_for(V);
+  auto waves_for = [&](int g) { return g >= 16 ? a.n_rows : (a.n_rows * g + kWave - 1) / kWave; };
+  while (V > 1 && waves_for(G) < kMinWaves) {
+    V >>= 1;
+    G = lanes_for(V);
+  }
   const int64_t slabs = (a.f + (int64_t)G * V - 1) / ((int64_t)G * V);
   const int64_t rows_per_block = G >= 16 ? kWavesPerBlock : (int64_t)kWavesPerBlock * (kWave / G);
   // one wave per row (wide) by default: measured best on products-synth (tools/tune.sh)
   static const int max_blocks = env_int("APPNP_MAX_BLOCKS", 1 << 30);
   int64_t blocks = (a.n_rows + rows_per_block - 1) / rows_per_block;
   if (blocks > max_blocks) blocks = max_blocks;
+  a.light_blocks = blocks;
+  if (G < 16 && a.heavy && a.n_heavy > 0) {
+    const int64_t hb = std::min<int64_t>((a.n_heavy + kWavesPerBlock - 1) / kWavesPerBlock, 4096);
+    blocks += hb;
+  } else {
+    a.heavy = nullptr;
+    a.n_heavy = 0;
+  }
   const dim3 grid((unsigned)blocks, (unsigned)slabs);
   if (dtype == 0) {
     switch (epi) {

@@ -506,11 +506,17 @@ def test_batch_topk_quirk_matches_batch_main(cora):
     adj = adj_of(cora)
     G = pa.Graph.from_scipy(adj, device=DEV)
     P = batch_topk_quirk(G, 128, K=200, alpha=0.1).cpu()
-    ref = torch.FloatTensor(O.compute_ppr(adj, alpha=0.1))
+    full = torch.FloatTensor(O.compute_ppr(adj, alpha=0.1))
+    ref = full.clone()
     thresh, _ = ref.topk(128, axis=-1)
     ref[ref < thresh[:, -1]] = 0
     kept, kept_ref = P > 0, ref > 0
-    assert (kept != kept_ref).float().mean() < 1e-4  # only near-ties may flip
+    # the fp64 PPR has exact ties at many k-th values; fp32 iteration breaks them by rounding,
+    # so entries may flip only where they sit within rounding distance of their threshold
+    flip = kept != kept_ref
+    gap = (full - thresh[:, -1][None, :]).abs()
+    assert (gap[flip] <= 1e-5 * full.abs().max()).all()
+    assert flip.float().mean() < 1e-3
     both = kept & kept_ref
     assert (P[both] - ref[both]).abs().max() <= 1e-5 * ref.abs().max()
 
@@ -612,3 +618,37 @@ def test_model_sparse_input_matches_dense(cora):
         a = model(Xd.to(DEV), idx)
         b = model(Xs, idx)
     assert torch.allclose(a, b, atol=1e-5, rtol=1e-4)
+
+
+# ---------------------------------------------------------------------------------------
+# power-law rows: hubs handled by whole wavefronts inside the narrow launch
+# ---------------------------------------------------------------------------------------
+
+
+def _hub_graph(n=4000, seed=0):
+    rng = np.random.default_rng(seed)
+    hubs = [0, 17, 999, n - 1]
+    src = np.concatenate([np.repeat(hubs, [3000, 500, 120, 33]),
+                          rng.integers(0, n, 6000)])
+    dst = np.concatenate([rng.integers(0, n, 3653), rng.integers(0, n, 6000)])
+    a = sp.coo_matrix((np.ones(len(src), np.float32), (src, dst)), shape=(n, n)).tocsr()
+    a = ((a + a.T) > 0).astype(np.float32).tocsr()
+    a.setdiag(0)
+    a.eliminate_zeros()
+    a.sort_indices()
+    return a
+
+
+@pytest.mark.parametrize("F", [3, 7, 16, 100])
+@pytest.mark.parametrize("p", [0.0, 0.3])
+def test_hub_rows_forward_backward(F, p):
+    pa = _lib()
+    adj = _hub_graph()
+    assert np.diff(adj.indptr).max() > 1000
+    G = pa.Graph.from_scipy(adj, device=DEV)
+    ah = O.calc_a_hat(adj, "sym")
+    H = torch.randn(adj.shape[0], F, generator=torch.Generator().manual_seed(F))
+    Z = to_np(pa.propagate_forward(G, H.to(DEV), 6, 0.1, p_drop=p, seed=4))
+    close_fp32(Z, O.appnp_propagate(ah, H.numpy(), 6, 0.1, p_drop=p, seed=4))
+    dH = to_np(pa.propagate_backward(G, H.to(DEV), 6, 0.1, p_drop=p, seed=4))
+    close_fp32(dH, O.appnp_backward(ah, H.numpy(), 6, 0.1, p_drop=p, seed=4))
