@@ -308,10 +308,20 @@ __global__ __launch_bounds__(kBlock) void k_step_narrow(StepArgs a) {
 }
 
 template <typename T, int V, int EPI, bool TAIL>
-hipError_t launch_g(int G, dim3 grid, const StepArgs& a, hipStream_t s) {
+hipError_t launch_g(int G, bool wide, dim3 grid, const StepArgs& a, hipStream_t s) {
   constexpr int UW = 4;  // entries in flight per sub-group (wide)
   constexpr int UN = 4;  // entries in flight per row (narrow)
   const dim3 block(kBlock);
+  if (wide && G < 16) {  // small graphs: a wavefront per row even for narrow rows
+    switch (G) {
+      case 1: hipLaunchKernelGGL((k_step_wide<T, V, 1, EPI, UW, TAIL>), grid, block, 0, s, a); break;
+      case 2: hipLaunchKernelGGL((k_step_wide<T, V, 2, EPI, UW, TAIL>), grid, block, 0, s, a); break;
+      case 4: hipLaunchKernelGGL((k_step_wide<T, V, 4, EPI, UW, TAIL>), grid, block, 0, s, a); break;
+      case 8: hipLaunchKernelGGL((k_step_wide<T, V, 8, EPI, UW, TAIL>), grid, block, 0, s, a); break;
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
   switch (G) {
     case 1: hipLaunchKernelGGL((k_step_narrow<T, V, 1, EPI, UN, TAIL>), grid, block, 0, s, a); break;
     case 2: hipLaunchKernelGGL((k_step_narrow<T, V, 2, EPI, UN, TAIL>), grid, block, 0, s, a); break;
@@ -326,18 +336,18 @@ hipError_t launch_g(int G, dim3 grid, const StepArgs& a, hipStream_t s) {
 }
 
 template <typename T, int EPI>
-hipError_t launch_v(int V, int G, dim3 grid, const StepArgs& a, hipStream_t s) {
+hipError_t launch_v(int V, int G, bool wide, dim3 grid, const StepArgs& a, hipStream_t s) {
   const bool tail = (a.f % V) != 0;
   switch (V) {
-    case 1: return launch_g<T, 1, EPI, false>(G, grid, a, s);
-    case 2: return tail ? launch_g<T, 2, EPI, true>(G, grid, a, s)
-                        : launch_g<T, 2, EPI, false>(G, grid, a, s);
-    case 4: return tail ? launch_g<T, 4, EPI, true>(G, grid, a, s)
-                        : launch_g<T, 4, EPI, false>(G, grid, a, s);
+    case 1: return launch_g<T, 1, EPI, false>(G, wide, grid, a, s);
+    case 2: return tail ? launch_g<T, 2, EPI, true>(G, wide, grid, a, s)
+                        : launch_g<T, 2, EPI, false>(G, wide, grid, a, s);
+    case 4: return tail ? launch_g<T, 4, EPI, true>(G, wide, grid, a, s)
+                        : launch_g<T, 4, EPI, false>(G, wide, grid, a, s);
     case 8:
       if constexpr (sizeof(T) == 2)
-        return tail ? launch_g<T, 8, EPI, true>(G, grid, a, s)
-                    : launch_g<T, 8, EPI, false>(G, grid, a, s);
+        return tail ? launch_g<T, 8, EPI, true>(G, wide, grid, a, s)
+                    : launch_g<T, 8, EPI, false>(G, wide, grid, a, s);
       return hipErrorInvalidValue;
     default: return hipErrorInvalidValue;
   }
@@ -378,23 +388,20 @@ hipError_t launch_step(int dtype, int epi, int V, const StepArgs& a_in, hipStrea
     while (g < need) g <<= 1;
     return g;
   };
-  // Small graphs are latency-bound: keep >= kMinWaves wavefronts in flight by narrowing the
-  // vector (more lanes per row, fewer rows per wave) before settling on V.
-  constexpr int64_t kMinWaves = 2048;
-  int G = lanes_for(V);
-  auto waves_for = [&](int g) { return g >= 16 ? a.n_rows : (a.n_rows * g + kWave - 1) / kWave; };
-  while (V > 1 && waves_for(G) < kMinWaves) {
-    V >>= 1;
-    G = lanes_for(V);
-  }
+  // Small graphs are latency-bound: there a wavefront per row (its entries staged once and
+  // gathered in one round by 64/G sub-groups) beats G-lane rows that walk their entries a
+  // few at a time; large graphs keep G-lane rows for narrow F (fewer instructions per byte).
+  constexpr int64_t kLatencyRows = 1 << 16;
+  const int G = lanes_for(V);
+  const bool wide = G >= 16 || a.n_rows <= kLatencyRows;
   const int64_t slabs = (a.f + (int64_t)G * V - 1) / ((int64_t)G * V);
-  const int64_t rows_per_block = G >= 16 ? kWavesPerBlock : (int64_t)kWavesPerBlock * (kWave / G);
+  const int64_t rows_per_block = wide ? kWavesPerBlock : (int64_t)kWavesPerBlock * (kWave / G);
   // one wave per row (wide) by default: measured best on products-synth (tools/tune.sh)
   static const int max_blocks = env_int("APPNP_MAX_BLOCKS", 1 << 30);
   int64_t blocks = (a.n_rows + rows_per_block - 1) / rows_per_block;
   if (blocks > max_blocks) blocks = max_blocks;
   a.light_blocks = blocks;
-  if (G < 16 && a.heavy && a.n_heavy > 0) {
+  if (!wide && a.heavy && a.n_heavy > 0) {
     const int64_t hb = std::min<int64_t>((a.n_heavy + kWavesPerBlock - 1) / kWavesPerBlock, 4096);
     blocks += hb;
   } else {
@@ -404,15 +411,15 @@ hipError_t launch_step(int dtype, int epi, int V, const StepArgs& a_in, hipStrea
   const dim3 grid((unsigned)blocks, (unsigned)slabs);
   if (dtype == 0) {
     switch (epi) {
-      case EPI_FWD: return launch_v<float, EPI_FWD>(V, G, grid, a, s);
-      case EPI_BWD: return launch_v<float, EPI_BWD>(V, G, grid, a, s);
-      case EPI_PARTIAL: return launch_v<float, EPI_PARTIAL>(V, G, grid, a, s);
-      case EPI_FINISH: return launch_v<float, EPI_FINISH>(V, G, grid, a, s);
+      case EPI_FWD: return launch_v<float, EPI_FWD>(V, G, wide, grid, a, s);
+      case EPI_BWD: return launch_v<float, EPI_BWD>(V, G, wide, grid, a, s);
+      case EPI_PARTIAL: return launch_v<float, EPI_PARTIAL>(V, G, wide, grid, a, s);
+      case EPI_FINISH: return launch_v<float, EPI_FINISH>(V, G, wide, grid, a, s);
     }
   } else {
     switch (epi) {
-      case EPI_FWD: return launch_v<uint16_t, EPI_FWD>(V, G, grid, a, s);
-      case EPI_BWD: return launch_v<uint16_t, EPI_BWD>(V, G, grid, a, s);
+      case EPI_FWD: return launch_v<uint16_t, EPI_FWD>(V, G, wide, grid, a, s);
+      case EPI_BWD: return launch_v<uint16_t, EPI_BWD>(V, G, wide, grid, a, s);
     }
   }
   return hipErrorInvalidValue;
