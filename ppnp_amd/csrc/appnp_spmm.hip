@@ -391,9 +391,18 @@ hipError_t launch_step(int dtype, int epi, int V, const StepArgs& a_in, hipStrea
   // Small graphs are latency-bound: there a wavefront per row (its entries staged once and
   // gathered in one round by 64/G sub-groups) beats G-lane rows that walk their entries a
   // few at a time; large graphs keep G-lane rows for narrow F (fewer instructions per byte).
+  // Latency regime (<= 64k rows, measured on pubmed/ms-academic/cora-sized graphs): one
+  // feature per lane (V = 1 while F <= 64) -- more lanes per row and a short sub-group
+  // reduction -- and a wavefront per row only when the graph has hub rows.
   constexpr int64_t kLatencyRows = 1 << 16;
+  const bool latency = a.n_rows <= kLatencyRows;
+  if (latency) {
+    int v = 1;
+    while (v < V && (int64_t)64 * v < a.f) v <<= 1;
+    V = v;
+  }
   const int G = lanes_for(V);
-  const bool wide = G >= 16 || a.n_rows <= kLatencyRows;
+  const bool wide = G >= 16 || (latency && a.heavy && a.n_heavy > 0);
   const int64_t slabs = (a.f + (int64_t)G * V - 1) / ((int64_t)G * V);
   const int64_t rows_per_block = wide ? kWavesPerBlock : (int64_t)kWavesPerBlock * (kWave / G);
   // one wave per row (wide) by default: measured best on products-synth (tools/tune.sh)
