@@ -348,7 +348,6 @@ int csr_transpose(const int32_t* indptr, const int32_t* indices, const float* va
                                                                            : APPNP_EDEVICE; \
   } while (0)
   Buffers b;
-  float* vtmp = nullptr;
   unsigned h_err = 0;
   out->n = cols;
   out->n_in = rows;
@@ -389,7 +388,6 @@ int csr_transpose(const int32_t* indptr, const int32_t* indices, const float* va
   TRY(hipGetLastError());
   TRY(hipMemcpyAsync(&h_err, b.flags, sizeof(h_err), hipMemcpyDeviceToHost, s));
   TRY(hipStreamSynchronize(s));
-  (void)vtmp;
   return h_err ? APPNP_EINVAL : APPNP_OK;
 #undef TRY
 }
