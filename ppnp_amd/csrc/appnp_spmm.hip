@@ -406,7 +406,9 @@ hipError_t launch_step(int dtype, int epi, int V, const StepArgs& a_in, hipStrea
   const int64_t slabs = (a.f + (int64_t)G * V - 1) / ((int64_t)G * V);
   const int64_t rows_per_block = wide ? kWavesPerBlock : (int64_t)kWavesPerBlock * (kWave / G);
   // one wave per row (wide) by default: measured best on products-synth (tools/tune.sh)
-  static const int max_blocks = env_int("APPNP_MAX_BLOCKS", 1 << 30);
+  // gridDim.x * 256 must stay below 2^32: cap at 4M blocks (grid-stride loops take the rest;
+  // products-synth needs 612k, i.e. one wave per row)
+  static const int max_blocks = std::min(env_int("APPNP_MAX_BLOCKS", 1 << 22), 1 << 22);
   int64_t blocks = (a.n_rows + rows_per_block - 1) / rows_per_block;
   if (blocks > max_blocks) blocks = max_blocks;
   a.light_blocks = blocks;
