@@ -192,6 +192,19 @@ int appnp_step(const appnp_graph* g, int part, const void* Zin, int64_t ld_in, c
                int64_t ld_partial, int64_t f, int dtype, int k, float alpha, float p_drop,
                uint64_t seed, void* stream);
 
+/*
+ * A captured propagation plan: the K launches of appnp_propagate for FIXED buffers (H, Z, ws)
+ * and parameters, recorded once into a hipGraph and replayed by appnp_plan_launch on any
+ * stream with a single graph launch.  For small, launch-bound graphs and serving loops that
+ * refill H in place.  Creating a plan captures on an internal stream (no kernels run).
+ */
+typedef struct appnp_plan appnp_plan;
+int appnp_plan_create(const appnp_graph* g, const void* H, int64_t ld_h, void* Z, int64_t ld_z,
+                      int64_t f, int dtype, int K, float alpha, float p_drop, uint64_t seed,
+                      void* ws, size_t ws_bytes, appnp_plan** out);
+int appnp_plan_launch(const appnp_plan* p, void* stream);
+void appnp_plan_destroy(appnp_plan* p);
+
 #ifdef __cplusplus
 }
 #endif

@@ -66,6 +66,13 @@ _SIGS = {
         _i32,
         [_vp, _vp, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _i64, _f32, _u64, _i32, _vp],
     ),
+    "appnp_plan_create": (
+        _i32,
+        [_vp, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _f32, _f32, _u64, _vp, _sz,
+         C.POINTER(_vp)],
+    ),
+    "appnp_plan_launch": (_i32, [_vp, _vp]),
+    "appnp_plan_destroy": (None, [_vp]),
     "appnp_step": (
         _i32,
         [_vp, _i32, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _f32,

@@ -412,4 +412,51 @@ int appnp_step(const appnp_graph* g, int part, const void* Zin, int64_t ld_in, c
   return dev_err(appnp::launch_step(dtype, epi, V, a, as_stream(stream)));
 }
 
+// ---- captured plans: the K launches of appnp_propagate replayed as one hipGraph -----------
+
+struct appnp_plan {
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+};
+
+int appnp_plan_create(const appnp_graph* g, const void* H, int64_t ld_h, void* Z, int64_t ld_z,
+                      int64_t f, int dtype, int K, float alpha, float p_drop, uint64_t seed,
+                      void* ws, size_t ws_bytes, appnp_plan** out) {
+  if (!out) return APPNP_EINVAL;
+  *out = nullptr;
+  hipStream_t cs = nullptr;
+  if (hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) != hipSuccess) return APPNP_EDEVICE;
+  appnp_plan* p = new (std::nothrow) appnp_plan();
+  if (!p) {
+    (void)hipStreamDestroy(cs);
+    return APPNP_ENOMEM;
+  }
+  int rc = dev_err(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
+  if (rc == APPNP_OK) {
+    rc = appnp_propagate(g, H, ld_h, Z, ld_z, f, dtype, K, alpha, p_drop, seed, ws, ws_bytes, cs);
+    const hipError_t e = hipStreamEndCapture(cs, &p->graph);  // always end the capture
+    if (rc == APPNP_OK) rc = dev_err(e);
+  }
+  if (rc == APPNP_OK) rc = dev_err(hipGraphInstantiate(&p->exec, p->graph, nullptr, nullptr, 0));
+  (void)hipStreamDestroy(cs);
+  if (rc != APPNP_OK) {
+    appnp_plan_destroy(p);
+    return rc;
+  }
+  *out = p;
+  return APPNP_OK;
+}
+
+int appnp_plan_launch(const appnp_plan* p, void* stream) {
+  if (!p || !p->exec) return APPNP_EINVAL;
+  return dev_err(hipGraphLaunch(p->exec, as_stream(stream)));
+}
+
+void appnp_plan_destroy(appnp_plan* p) {
+  if (!p) return;
+  if (p->exec) (void)hipGraphExecDestroy(p->exec);
+  if (p->graph) (void)hipGraphDestroy(p->graph);
+  delete p;
+}
+
 }  // extern "C"

@@ -120,3 +120,45 @@ def step(graph: Graph, Zin: torch.Tensor, H: torch.Tensor, out: torch.Tensor, k:
                             float(p_drop), int(seed) & (2**64 - 1), _stream(graph.device))
     _lib.check("appnp_step", rc)
     return out
+
+
+class PropagatePlan:
+    """A captured propagation (``appnp_plan_create``): K launches recorded once into a hipGraph
+    for fixed H / Z buffers, replayed with one graph launch.  Refill ``plan.H`` in place, call
+    ``plan()``, read ``plan.Z``.  For small, launch-bound graphs and serving loops."""
+
+    def __init__(self, graph: Graph, H: torch.Tensor, K: int = 10, alpha: float = 0.1,
+                 p_drop: float = 0.0, seed: int = 0):
+        _check_dense("H", H, graph, graph.n)
+        self.graph, self.H = graph, H
+        self.Z = torch.empty_like(H, memory_format=torch.contiguous_format)
+        lib = _lib.load()
+        dt = _DTYPES[H.dtype]
+        f = int(H.shape[1])
+        self._ws_bytes = int(lib.appnp_workspace_bytes(graph.handle, f, _ld(self.Z), dt))
+        self._ws = torch.empty(max(self._ws_bytes, 1), dtype=torch.uint8, device=graph.device)
+        self._p = C.c_void_p()
+        torch.cuda.current_stream(graph.device).synchronize()  # buffers allocated before capture
+        with torch.cuda.device(graph.device):
+            rc = lib.appnp_plan_create(graph.handle, _vp(H), _ld(H), _vp(self.Z), _ld(self.Z), f,
+                                       dt, int(K), float(alpha), float(p_drop),
+                                       int(seed) & (2**64 - 1), _vp(self._ws), self._ws_bytes,
+                                       C.byref(self._p))
+        _lib.check("appnp_plan_create", rc)
+
+    def __call__(self) -> torch.Tensor:
+        with torch.cuda.device(self.graph.device):
+            rc = _lib.load().appnp_plan_launch(self._p, _stream(self.graph.device))
+        _lib.check("appnp_plan_launch", rc)
+        return self.Z
+
+    def close(self):
+        if getattr(self, "_p", None):
+            _lib.load().appnp_plan_destroy(self._p)
+            self._p = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -652,3 +652,20 @@ def test_hub_rows_forward_backward(F, p):
     close_fp32(Z, O.appnp_propagate(ah, H.numpy(), 6, 0.1, p_drop=p, seed=4))
     dH = to_np(pa.propagate_backward(G, H.to(DEV), 6, 0.1, p_drop=p, seed=4))
     close_fp32(dH, O.appnp_backward(ah, H.numpy(), 6, 0.1, p_drop=p, seed=4))
+
+
+def test_plan_replay_matches_propagate():
+    """appnp_plan_*: the captured K-launch graph gives bitwise the eager result, and replays
+    pick up in-place refills of H."""
+    from ppnp_amd.ops import PropagatePlan
+
+    pa = _lib()
+    adj = synth(6000, 30000, seed=12)
+    G = pa.Graph.from_scipy(adj, device=DEV)
+    H = torch.randn(6000, 12, generator=torch.Generator().manual_seed(1)).to(DEV)
+    plan = PropagatePlan(G, H, K=10, alpha=0.1)
+    assert torch.equal(plan().clone(), pa.propagate_forward(G, H, 10, 0.1))
+    H.mul_(-2.0)
+    torch.cuda.synchronize()
+    assert torch.equal(plan().clone(), pa.propagate_forward(G, H, 10, 0.1))
+    plan.close()
