@@ -54,6 +54,9 @@ def parse():
     p.add_argument("--emulate", default=None, metavar="P:r",
                    help="single-GPU emulation of rank r of a P-rank --layout (kernel time of "
                         "that rank only, no exchange; NOT a multi-GPU result)")
+    p.add_argument("--plan", action="store_true",
+                   help="single GPU: replay the K launches as one captured hipGraph "
+                        "(appnp_plan_*; for small, launch-bound workloads)")
     p.add_argument("--overlap", action="store_true",
                    help="row layouts: overlap the all-gather with the local-column product")
     return p.parse_args()
@@ -171,8 +174,17 @@ def main():
         t_build = time.perf_counter() - t1
         Z = torch.empty(n, ld, dtype=dtype, device=dev)[:, :F]
 
-        def run():
-            ppnp_amd.propagate_forward(graph, H, K, alpha, out=Z)
+        if args.plan:
+            from ppnp_amd.ops import PropagatePlan
+
+            plan = PropagatePlan(graph, H, K, alpha)
+
+            def run():
+                plan()
+        else:
+
+            def run():
+                ppnp_amd.propagate_forward(graph, H, K, alpha, out=Z)
 
         stream = torch.cuda.current_stream(dev)
         F_local = F
