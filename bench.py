@@ -47,7 +47,7 @@ def parse():
     p.add_argument("--workload", default="products-synth")
     p.add_argument("--dtype", default=None, choices=["f32", "bf16"],
                    help="override the workload's storage dtype (non-headline variants)")
-    p.add_argument("--cpu-iters", type=int, default=2,
+    p.add_argument("--cpu-iters", type=int, default=10,
                    help="iterations of the CPU baseline sample (0 disables it)")
     p.add_argument("--layout", default="auto",
                    help="multi-GPU layout: auto | row | col | RxC (row groups x column groups)")
