@@ -66,11 +66,12 @@ void set_drop(StepArgs& a, float p_drop, uint64_t seed, int k) {
     a.mkey = appnp::splitmix64(seed + (uint64_t)(k + 1) * 0x9E3779B97F4A7C15ull);
     double thr = (double)p_drop * (double)(1u << 24);
     a.drop_thr = (uint32_t)thr;
-    if (a.drop_thr == 0u) a.drop_thr = 0u;
+    a.drop_on = 1;  // even when the 24-bit threshold rounds to 0, kept edges are rescaled
     a.drop_scale = 1.0f / (1.0f - p_drop);
   } else {
     a.mkey = 0;
     a.drop_thr = 0u;
+    a.drop_on = 0;
     a.drop_scale = 1.0f;
   }
 }

@@ -33,7 +33,8 @@ struct StepArgs {
   int64_t row_lo;          // global index of local row 0 (hash key only)
   uint64_t mkey;           // per-iteration dropout key = splitmix64(seed + (k+1)*golden)
   int32_t f;               // features
-  uint32_t drop_thr;       // 24-bit drop threshold; 0 = no dropout
+  uint32_t drop_thr;       // 24-bit drop threshold (edge dropped iff hash24 < drop_thr)
+  int32_t drop_on;         // 1 when p_drop > 0
   float scale;             // 1 - alpha
   float alpha;             // weight of H (FWD/FINISH) or of y into aux (BWD)
   float drop_scale;        // 1 / (1 - p)
@@ -57,7 +58,7 @@ __host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
 // edge_keep_mask.  Independent of the partition and of the visiting order.
 __device__ __forceinline__ float edge_weight(float w, int64_t grow, int32_t c,
                                              const StepArgs& a) {
-  if (a.drop_thr == 0u) return w;
+  if (!a.drop_on) return w;
   const uint64_t r = (uint32_t)grow, cc = (uint32_t)c;
   const uint64_t key = a.tkey ? ((cc << 32) | r) : ((r << 32) | cc);
   const uint64_t h = splitmix64(key ^ a.mkey);

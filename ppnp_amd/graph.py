@@ -30,10 +30,9 @@ class Graph:
     Build it with :meth:`from_scipy` (host CSR) or :meth:`from_csr` (torch CSR arrays).
     """
 
-    def __init__(self, handle, device, keep_alive=()):
+    def __init__(self, handle, device):
         self._h = handle
         self.device = torch.device(device)
-        self._keep = keep_alive
         lib = _lib.load()
         n, lo, hi, nnz = C.c_int64(), C.c_int64(), C.c_int64(), C.c_int64()
         mode, sym = C.c_int(), C.c_int()

@@ -68,7 +68,8 @@ def propagate_forward(graph: Graph, H: torch.Tensor, K: int, alpha: float, p_dro
 
 def propagate_backward(graph: Graph, dZ: torch.Tensor, K: int, alpha: float, p_drop: float = 0.0,
                        seed: int = 0) -> torch.Tensor:
-    """dH = J^T dZ via ``appnp_propagate_bwd`` (symmetric 'sym' graphs)."""
+    """dH = J^T dZ via ``appnp_propagate_bwd`` (A_hat^T: A_hat itself for 'sym' on an
+    undirected graph, else the transpose built with ``Graph(..., transpose=True)``)."""
     dZ = dZ.contiguous()
     _check_dense("dZ", dZ, graph, graph.n)
     dH = torch.empty_like(dZ)
