@@ -141,7 +141,7 @@ def main():
     ctl_dev = dev if world > 1 and torch.distributed.get_backend() == "nccl" else "cpu"
 
     t0 = time.perf_counter()
-    indptr, indices = synth.uniform_graph_device(n, m, seed, device=dev)
+    indptr, indices = synth.graph_for(args.workload, device=dev)
     H = synth.features(n, F, dtype=dtype, device=dev)
     esz = 2 if dtype == torch.bfloat16 else 4
     ld = pdist.line_ld(F, esz)

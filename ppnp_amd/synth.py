@@ -21,9 +21,13 @@ CONFIGS = {
     "ms-academic-synth": (18333, 81894, 15, 20, 0.2, torch.bfloat16),
     "arxiv-synth": (169343, 1166243, 128, 10, 0.1, torch.float32),
     "products-synth": (2449029, 61859140, 100, 10, 0.1, torch.float32),
+    # power-law stand-in (SURVEY 8(d) "optionally add a Chung-Lu power-law variant")
+    "products-powerlaw": (2449029, 61859140, 100, 10, 0.1, torch.float32),
 }
 
-SEEDS = {"pubmed-synth": 1, "ms-academic-synth": 2, "arxiv-synth": 3, "products-synth": 4}
+SEEDS = {"pubmed-synth": 1, "ms-academic-synth": 2, "arxiv-synth": 3, "products-synth": 4,
+         "products-powerlaw": 5}
+POWERLAW = {"products-powerlaw"}
 
 
 def uniform_graph_device(n: int, m: int, seed: int, device="cuda"):
@@ -44,6 +48,43 @@ def uniform_graph_device(n: int, m: int, seed: int, device="cuda"):
     indptr = torch.zeros(n + 1, dtype=torch.int64, device=device)
     indptr[1:] = torch.cumsum(counts, 0)
     return indptr.to(torch.int32), col
+
+
+def chung_lu_graph_device(n: int, m: int, seed: int, exponent: float = 3.2,
+                          device="cuda"):
+    """Power-law graph (Chung-Lu): endpoints drawn with probability proportional to
+    w_i = (i + 1)^(-1/(exponent-1)) (inverse-CDF sampling), then the same symmetrise /
+    de-duplicate / no-self-loop steps as ``uniform_graph_device``.  Exponent 3.2 gives a
+    largest degree of ~20k at products scale (the real ogbn-products: ~17k, mean ~50)."""
+    g = torch.Generator(device=device).manual_seed(seed)
+    w = torch.arange(1, n + 1, device=device, dtype=torch.float64).pow(-1.0 / (exponent - 1.0))
+    cdf = torch.cumsum(w, 0)
+    cdf /= cdf[-1].clone()
+    u = torch.rand(2, m, device=device, generator=g, dtype=torch.float64)
+    ends = torch.searchsorted(cdf, u).clamp_(max=n - 1)
+    # scatter node ids so hubs are not all at low indices
+    perm = torch.randperm(n, device=device, generator=g)
+    src, dst = perm[ends[0]], perm[ends[1]]
+    del ends, u, cdf, w
+    keep = src != dst
+    src, dst = src[keep], dst[keep]
+    key = torch.cat([src * n + dst, dst * n + src])
+    del src, dst, keep
+    key = torch.unique(key, sorted=True)
+    row = torch.div(key, n, rounding_mode="floor")
+    col = (key - row * n).to(torch.int32)
+    del key
+    counts = torch.bincount(row, minlength=n)
+    indptr = torch.zeros(n + 1, dtype=torch.int64, device=device)
+    indptr[1:] = torch.cumsum(counts, 0)
+    return indptr.to(torch.int32), col
+
+
+def graph_for(workload: str, device="cuda"):
+    n, m = CONFIGS[workload][:2]
+    if workload in POWERLAW:
+        return chung_lu_graph_device(n, m, SEEDS[workload], device=device)
+    return uniform_graph_device(n, m, SEEDS.get(workload, 0), device=device)
 
 
 def features(n: int, f: int, dtype=torch.float32, device="cuda", seed: int = 0):
