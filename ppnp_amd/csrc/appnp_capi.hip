@@ -99,6 +99,8 @@ StepArgs base_args(const appnp_graph* g, int64_t f, float alpha) {
   a.heavy = g->heavy;
   a.n_heavy = g->n_heavy;
   a.heavy_thr = appnp::kHeavyRow;
+  a.hub = g->hub;
+  a.n_hub = g->n_hub;
   return a;
 }
 
@@ -306,6 +308,8 @@ int appnp_propagate_bwd(const appnp_graph* g, const void* dZ, int64_t ld_dz, voi
     a.val = g->t_val;
     a.heavy = g->t_heavy;
     a.n_heavy = g->t_n_heavy;
+    a.hub = g->t_hub;
+    a.n_hub = g->t_n_hub;
   }
   a.tkey = 1;  // entry (j, i) of A_hat^T carries the mask of forward edge (i, j)
   a.aux = dH;
@@ -387,8 +391,10 @@ int appnp_step(const appnp_graph* g, int part, const void* Zin, int64_t ld_in, c
   } else {
     if (!g->split) return APPNP_EINVAL;
     if (dtype != APPNP_F32) return APPNP_ENOTSUP;
-    a.heavy = nullptr;  // the heavy-row list describes the full rows, not their halves
+    a.heavy = nullptr;  // the heavy/hub lists describe the full rows, not their halves
     a.n_heavy = 0;
+    a.hub = nullptr;
+    a.n_hub = 0;
     if (part == APPNP_PART_LOCAL) {
       epi = appnp::EPI_PARTIAL;
       a.row_ptr = g->lrow_ptr;

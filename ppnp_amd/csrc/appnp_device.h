@@ -43,9 +43,12 @@ struct StepArgs {
   int64_t n_heavy;
   int32_t heavy_thr;
   int64_t light_blocks;    // set by launch_step: blocks [light_blocks, grid) take heavy rows
+  const int32_t* hub;      // rows longer than kHubRow: the wide kernels dispatch them first
+  int64_t n_hub;
 };
 
-constexpr int kHeavyRow = 32;  // a row longer than this gets a whole wavefront
+constexpr int kHeavyRow = 32;   // a row longer than this gets a whole wavefront (narrow)
+constexpr int kHubRow = 512;    // ... and one longer than this is dispatched first (wide)
 
 __host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
   x += 0x9E3779B97F4A7C15ull;

@@ -268,9 +268,10 @@ __global__ __launch_bounds__(kBlock) void k_heavy_scatter(const int32_t* __restr
 
 }  // namespace
 
-// Ascending list of the rows with more than kHeavyRow entries (load balance of the narrow
-// kernels on power-law graphs).  Synchronises (setup only).
-int build_heavy(const int32_t* rp, int64_t rows, hipStream_t s, int32_t** out, int64_t* n_out) {
+// Ascending list of the rows with more than `thr` entries (load balance on power-law graphs:
+// kHeavyRow for the narrow kernels, kHubRow for hub-first dispatch).  Synchronises (setup).
+int build_heavy(const int32_t* rp, int64_t rows, int32_t thr, hipStream_t s, int32_t** out,
+                int64_t* n_out) {
   *out = nullptr;
   *n_out = 0;
   if (rows <= 0) return APPNP_OK;
@@ -285,7 +286,7 @@ int build_heavy(const int32_t* rp, int64_t rows, hipStream_t s, int32_t** out, i
       hipMalloc(&tot, sizeof(int64_t)) != hipSuccess) {
     rc = APPNP_ENOMEM;
   } else {
-    hipLaunchKernelGGL(k_heavy_flags, dim3(grid), dim3(kBlock), 0, s, rp, rows, kHeavyRow, flag);
+    hipLaunchKernelGGL(k_heavy_flags, dim3(grid), dim3(kBlock), 0, s, rp, rows, thr, flag);
     if (exclusive_scan(flag, rows, pos, bsum, tot, s) != hipSuccess ||
         hipMemcpyAsync(&h_tot, tot, sizeof(int64_t), hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess) {
@@ -311,7 +312,7 @@ void graph_free(appnp_graph* g) {
   if (!g) return;
   void* ptrs[] = {g->row_ptr, g->col, g->val, g->lrow_ptr, g->lcol, g->lval,
                   g->rrow_ptr, g->rcol, g->rval, g->dinv, g->t_row_ptr, g->t_col, g->t_val,
-                  g->heavy, g->t_heavy};
+                  g->heavy, g->t_heavy, g->hub, g->t_hub};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   g->row_ptr = g->col = g->lrow_ptr = g->lcol = g->rrow_ptr = g->rcol = nullptr;
@@ -319,7 +320,7 @@ void graph_free(appnp_graph* g) {
   g->dinv = nullptr;
   g->t_row_ptr = g->t_col = nullptr;
   g->t_val = nullptr;
-  g->heavy = g->t_heavy = nullptr;
+  g->heavy = g->t_heavy = g->hub = g->t_hub = nullptr;
 }
 
 #define APPNP_TRY(expr)                                                         \
@@ -419,7 +420,8 @@ int graph_build(const int32_t* indptr, const int32_t* indices, const float* vals
   }
   APPNP_TRY(hipStreamSynchronize(s));
   (void)nnz;
-  rc = build_heavy(g->row_ptr, rows, s, &g->heavy, &g->n_heavy);
+  rc = build_heavy(g->row_ptr, rows, kHeavyRow, s, &g->heavy, &g->n_heavy);
+  if (rc == APPNP_OK) rc = build_heavy(g->row_ptr, rows, kHubRow, s, &g->hub, &g->n_hub);
 
 done:
   if (cnt) (void)hipFree(cnt);

@@ -404,7 +404,9 @@ int graph_build_transpose(appnp_graph* g, hipStream_t s) {
   g->t_col = t.indices;
   g->t_val = t.data;
   if (t.node_map) (void)hipFree(t.node_map);
-  return build_heavy(g->t_row_ptr, g->n, s, &g->t_heavy, &g->t_n_heavy);
+  int rc2 = build_heavy(g->t_row_ptr, g->n, kHeavyRow, s, &g->t_heavy, &g->t_n_heavy);
+  if (rc2 == APPNP_OK) rc2 = build_heavy(g->t_row_ptr, g->n, kHubRow, s, &g->t_hub, &g->t_n_hub);
+  return rc2;
 }
 
 void csr_free(appnp_csr* c) {

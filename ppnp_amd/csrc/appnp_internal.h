@@ -30,6 +30,10 @@ struct appnp_graph {
   int64_t n_heavy = 0;
   int32_t* t_heavy = nullptr;   // the same for A_hat^T
   int64_t t_n_heavy = 0;
+  int32_t* hub = nullptr;       // rows with > kHubRow entries: dispatched first (wide kernels)
+  int64_t n_hub = 0;
+  int32_t* t_hub = nullptr;
+  int64_t t_n_hub = 0;
   int32_t* t_row_ptr = nullptr; // A_hat^T (APPNP_GRAPH_TRANSPOSE, when A_hat is not symmetric)
   int32_t* t_col = nullptr;
   float* t_val = nullptr;
@@ -45,7 +49,8 @@ int graph_build(const int32_t* indptr, const int32_t* indices, const float* vals
                 hipStream_t s, appnp_graph* g);
 void graph_free(appnp_graph* g);
 int graph_build_transpose(appnp_graph* g, hipStream_t s);
-int build_heavy(const int32_t* rp, int64_t rows, hipStream_t s, int32_t** out, int64_t* n_out);
+int build_heavy(const int32_t* rp, int64_t rows, int32_t thr, hipStream_t s, int32_t** out,
+                int64_t* n_out);
 int64_t scan_partials(int64_t rows);
 
 // appnp_ingest.hip

@@ -230,8 +230,20 @@ __global__ __launch_bounds__(kBlock) void k_step_wide(StepArgs a) {
   const int col0 = blockIdx.y * (G * V) + (lane % G) * V;
   const int rem = a.f - col0;  // valid features of this lane's fragment (>= V: full)
   const int64_t nwaves = (int64_t)gridDim.x * kWavesPerBlock;
-  for (int64_t row = (int64_t)blockIdx.x * kWavesPerBlock + wave; row < a.n_rows; row += nwaves)
+  // Longest-first dispatch: virtual rows [0, n_hub) are the hub rows (> kHubRow entries), so
+  // the longest waves start first and do not become the launch's tail; the regular pass
+  // skips them.  Pure scheduling: each row is still computed by exactly one wave.
+  const int64_t total = a.n_rows + a.n_hub;
+  for (int64_t v = (int64_t)blockIdx.x * kWavesPerBlock + wave; v < total; v += nwaves) {
+    int64_t row;
+    if (v < a.n_hub) {
+      row = a.hub[v];
+    } else {
+      row = v - a.n_hub;
+      if (a.hub && a.row_ptr[row + 1] - a.row_ptr[row] > kHubRow) continue;
+    }
     wave_row<T, V, G, EPI, U, TAIL>(a, row, lane, stage[wave], col0, rem);
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -409,7 +421,11 @@ hipError_t launch_step(int dtype, int epi, int V, const StepArgs& a_in, hipStrea
   // gridDim.x * 256 must stay below 2^32: cap at 4M blocks (grid-stride loops take the rest;
   // products-synth needs 612k, i.e. one wave per row)
   static const int max_blocks = std::min(env_int("APPNP_MAX_BLOCKS", 1 << 22), 1 << 22);
-  int64_t blocks = (a.n_rows + rows_per_block - 1) / rows_per_block;
+  if (!wide || !a.hub) {
+    a.hub = nullptr;
+    a.n_hub = 0;
+  }
+  int64_t blocks = (a.n_rows + a.n_hub + rows_per_block - 1) / rows_per_block;
   if (blocks > max_blocks) blocks = max_blocks;
   a.light_blocks = blocks;
   if (!wide && a.heavy && a.n_heavy > 0) {
