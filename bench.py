@@ -7,9 +7,11 @@ A "step" is one full propagation call -- K=10 fused SpMM+AXPBY iterations over t
 graph (appnp_propagate, or the row-partitioned multi-GPU loop) -- on synthetic input that is
 resident in HBM before the timed region.  value = nodes * F * K * steps / time (whole job).
 
-N > 1 (launched by torch.distributed.run, one rank per GPU): the node set is row-partitioned
-across ranks and Z is RCCL all-gathered every iteration; the timed
-region is bracketed by barrier + synchronize and the max over ranks is reported.
+N > 1 (launched by torch.distributed.run, one rank per GPU): the ranks form an R x C layout
+(ppnp_amd/dist.py): C feature slabs need no exchange, R row groups
+exchange their Z shards over RCCL every iteration.  --layout auto times the candidate layouts
+of ppnp_amd.dist.candidate_layouts after warm-up (max over ranks) and keeps the fastest; the
+timed region is bracketed by barrier + synchronize and the max over ranks is reported.
 
 Extra JSON fields:
   roofline      HBM roofline of the dominant kernel (k_step_*): algorithmic bytes per launch
@@ -59,6 +61,9 @@ def parse():
                         "(appnp_plan_*; for small, launch-bound workloads)")
     p.add_argument("--overlap", action="store_true",
                    help="row layouts: overlap the all-gather with the local-column product")
+    p.add_argument("--exchange", default="multipath", choices=["multipath", "group"],
+                   help="R x C layouts: relayed exchange over every rank, or one all-gather "
+                        "per column group")
     return p.parse_args()
 
 
@@ -100,6 +105,37 @@ def cpu_baseline(graph, H, K, alpha, iters):
     }
 
 
+def tune_layouts(cands, indptr, indices, n, H, K, alpha, dev, ctl_dev, reps=2):
+    """Build each candidate layout, time ``reps`` propagations after one warm-up (barrier on
+    both sides, max over ranks: every rank sees the same numbers and picks the same layout),
+    keep the fastest and free the others."""
+    from ppnp_amd import dist as pdist
+
+    best, best_ms, times = None, None, {}
+    for layout, overlap, exchange in cands:
+        r = pdist.PartitionedAPPNP.create(indptr, indices, n, H, K, alpha, dev, layout=layout,
+                                          overlap=overlap, exchange=exchange)
+        r.run()
+        torch.cuda.synchronize()
+        torch.distributed.barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            r.run()
+        torch.cuda.synchronize()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=ctl_dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        ms = float(t.item()) * 1e3 / reps
+        name = (f"rows{layout.rows}xcols{layout.cols}" + ("-overlap" if overlap else "")
+                + (f"-{exchange}" if layout.rows > 1 and layout.cols > 1 else ""))
+        times[name] = ms
+        if best_ms is None or ms < best_ms:
+            best, best_ms = r, ms
+        else:
+            del r
+        torch.cuda.empty_cache()
+    return best, times
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -128,12 +164,17 @@ def main():
         P, r = (int(x) for x in args.emulate.split(":"))
         emu = dict(rank=r, world=P, comm=pdist.NullComm())
         lw = P
-    layout = (pdist.choose_layout(lw, n, F, m) if args.layout == "auto"
-              else pdist.Layout.parse(args.layout, lw))
+    if args.layout == "auto" and world > 1 and not args.emulate:
+        cands = pdist.candidate_layouts(world, F)
+    else:
+        layout = (pdist.choose_layout(lw, n, F, m) if args.layout == "auto"
+                  else pdist.Layout.parse(args.layout, lw))
+        cands = [(layout, args.overlap, args.exchange)]
     if world > 1:
-        # RCCL only where the layout has a data-path exchange (row groups); a pure column
-        # layout has none, so its control plane (barrier, max-over-ranks) runs over gloo
-        backend = os.environ.get("PPNP_DIST_BACKEND") or ("nccl" if layout.rows > 1 else "gloo")
+        # RCCL only where a layout has a data-path exchange (row groups); pure column layouts
+        # have none, so their control plane (barrier, max-over-ranks) runs over gloo
+        rows = any(c[0].rows > 1 for c in cands)
+        backend = os.environ.get("PPNP_DIST_BACKEND") or ("nccl" if rows else "gloo")
         if backend == "nccl":
             torch.distributed.init_process_group("nccl", device_id=dev)
         else:
@@ -152,10 +193,16 @@ def main():
     torch.cuda.synchronize()
     t_gen = time.perf_counter() - t0
 
+    autotune = None
     if distributed:
         t1 = time.perf_counter()
-        runner = pdist.PartitionedAPPNP.create(indptr, indices, n, H, K, alpha, dev,
-                                               layout=layout, overlap=args.overlap, **emu)
+        if len(cands) == 1:
+            layout, overlap, exchange = cands[0]
+            runner = pdist.PartitionedAPPNP.create(indptr, indices, n, H, K, alpha, dev,
+                                                   layout=layout, overlap=overlap,
+                                                   exchange=exchange, **emu)
+        else:
+            runner, autotune = tune_layouts(cands, indptr, indices, n, H, K, alpha, dev, ctl_dev)
         torch.cuda.synchronize()
         t_build = time.perf_counter() - t1
         graph = runner.graph
@@ -233,9 +280,12 @@ def main():
     line_rate = lines / (avg_launch_ms * 1e-3) / 1e9
     value = n * F * K * args.steps / wall
     parallelism = ((f"rows{runner.layout.rows}xcols{runner.layout.cols}"
-                    + ("-overlap" if args.overlap else "")
+                    + ("-overlap" if runner.overlap else "")
+                    + (f"-{runner.exchange}" if runner.layout.rows > 1 and runner.layout.cols > 1
+                       else "")
                     + (f"-EMULATED-rank{args.emulate}" if args.emulate else ""))
                    if distributed else "single")
+    traffic = committed_traffic(args.workload, dtype, parallelism)
     res = {
         "metric": METRIC,
         "value": value,
@@ -266,9 +316,14 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
-            "traffic": committed_traffic(args.workload, dtype, parallelism),
+            "traffic": traffic,
             "traffic_source": "profiles/pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE / "
                               "WRITE_SIZE passes of this bench command, gfx950-corrected)",
+            # the PMC bytes per launch over the same launch time: how fast the kernel moves
+            # the bytes the random gathers force it to move (Infinity-Cache hits included)
+            "traffic_GBs": (traffic / (avg_launch_ms * 1e-3) / 1e9) if traffic else None,
+            "traffic_frac": (traffic / (avg_launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS)
+                            if traffic else None,
             "gather_line_rate": {
                 "lines_per_launch": lines,
                 "achieved_G_lines_s": line_rate,
@@ -281,6 +336,8 @@ def main():
             "avg_launch_ms": avg_launch_ms,
         },
     }
+    if autotune is not None:
+        res["config"]["autotune_ms_per_step"] = autotune
     if world == 1 and args.cpu_iters > 0:
         res["cpu_baseline"] = cpu_baseline(graph, H, K, alpha, args.cpu_iters)
     if rank == 0:

@@ -128,6 +128,166 @@ class _TorchComm:
         return None
 
 
+def _pieces(rows: int, parts: int):
+    """Row bounds of ``parts`` near-equal pieces of a shard of ``rows`` rows."""
+    return [col_range(rows, parts, t) for t in range(parts)]
+
+
+class _StreamDone:
+    """Handle of a side-stream exchange: wait() orders the caller's current stream after it."""
+
+    def __init__(self, event):
+        self.event = event
+
+    def wait(self):
+        if self.event is not None:
+            torch.cuda.current_stream().wait_event(self.event)
+
+
+class MultipathComm:
+    """All-gather of row shards within each column group, routed over every rank (RCCL P2P).
+
+    In an R x C layout (C > 1) the ranks of one column group only need each other's shards,
+    so a plain group all-gather drives R-1 of a GPU's 7 xGMI links and leaves the others idle
+    (2 x 4 on 8 GPUs: one link carries the whole shard).  Here every shard S is cut into P-1
+    pieces, one per other rank (the relay), in two batched P2P stages:
+
+    1. rank a sends piece_b(S_a) to every b != a.  A relay in a's column group keeps it in place;
+       any other relay parks it in a staging buffer.
+    2. every relay b forwards each parked piece_b(S_a) to the members of a's column group, and a
+       relay inside that group forwards to the other members (R > 2).
+
+    Per link and stage this moves S/(P-1) bytes (stage 2: (R-1) S/(P-1)) instead of S on R-1
+    links: on 2 x 4, 2 S/7 over all seven links instead of S over one.  P2P messages carry the
+    originating rank as tag, and both sides walk origins in ascending order (RCCL matches P2P
+    in issue order per peer pair, gloo by tag).
+
+    On 'nccl' the two stages run on a side stream that waits for the producer, so the caller's
+    stream stays free for the local-column product (overlap mode); the returned handle's wait()
+    orders the caller's stream after the exchange.  On 'gloo' (CPU tests, single-GPU
+    rehearsal) the exchange is synchronous and stages CUDA data through host memory.
+    """
+
+    def __init__(self, layout: Layout, rank: int):
+        self.layout, self.rank = layout, rank
+        self.P = layout.size
+        self.ri, self.ci = layout.coords(rank)
+        self.backend = dist.get_backend() if dist.is_initialized() else None
+        self._stream = None
+        self._staging = None
+
+    # ranks of a's column group
+    def group_of(self, a: int):
+        R = self.layout.rows
+        c = a // R
+        return [c * R + r for r in range(R)]
+
+    def relays(self, a: int):
+        return [b for b in range(self.P) if b != a]
+
+    def plan(self, shard_rows: int):
+        """(stage-1 ops, stage-2 ops) as lists of (kind, peer, origin, row range in the
+        origin's shard, 'full' | ('stage', slot)) for this rank."""
+        me, P = self.rank, self.P
+        mygroup = set(self.group_of(me))
+        pieces = _pieces(shard_rows, P - 1)
+        slots = {}
+        s1, s2 = [], []
+        for t, b in enumerate(self.relays(me)):  # my shard, piece t -> relay b
+            s1.append(("send", b, me, pieces[t], "full"))
+        for a in range(P):
+            if a == me:
+                continue
+            t = self.relays(a).index(me)  # the piece of S_a that I relay
+            if a in mygroup:
+                s1.append(("recv", a, a, pieces[t], "full"))
+                for c in self.group_of(a):
+                    if c not in (a, me):
+                        s2.append(("send", c, a, pieces[t], "full"))
+            else:
+                slot = slots.setdefault(a, len(slots))
+                s1.append(("recv", a, a, pieces[t], ("stage", slot)))
+                for c in self.group_of(a):
+                    if c != a:
+                        s2.append(("send", c, a, pieces[t], ("stage", slot)))
+        for a in sorted(mygroup - {me}):  # the rest of S_a reaches me through the relays
+            for tb, b in enumerate(self.relays(a)):
+                if b != me:
+                    s2.append(("recv", b, a, pieces[tb], "full"))
+        return s1, s2, len(slots), max((hi - lo for lo, hi in pieces), default=0)
+
+    def _views(self, full, shard_rows, ops, nslots, pmax):
+        R = self.layout.rows
+        if nslots and (self._staging is None or self._staging.shape[1:] != (pmax, full.shape[1])
+                       or self._staging.dtype != full.dtype
+                       or self._staging.device != full.device):
+            self._staging = torch.empty(nslots, pmax, full.shape[1], dtype=full.dtype,
+                                        device=full.device)
+        out = []
+        for kind, peer, origin, (lo, hi), where in ops:
+            if where == "full":
+                base = (origin % R) * shard_rows
+                t = full[base + lo:base + hi]
+            else:
+                t = self._staging[where[1], :hi - lo]
+            out.append((kind, peer, origin, t))
+        return out
+
+    def _run_stage(self, views, host):
+        ops = []
+        bufs = []
+        for kind, peer, origin, t in views:
+            if t.shape[0] == 0:
+                continue
+            buf = t
+            if host:
+                buf = t.detach().to("cpu", copy=True) if kind == "send" else torch.empty(
+                    t.shape, dtype=t.dtype)
+                bufs.append((kind, t, buf))
+            fn = dist.isend if kind == "send" else dist.irecv
+            if self.backend == "nccl":
+                ops.append(dist.P2POp(fn, buf, peer, tag=origin))
+            else:
+                ops.append(fn(buf, peer, tag=origin))
+        if self.backend == "nccl":
+            works = dist.batch_isend_irecv(ops) if ops else []
+        else:
+            works = ops
+        for w in works:
+            w.wait()
+        for kind, t, buf in bufs:
+            if kind == "recv":
+                t.copy_(buf)
+
+    def all_gather_rows(self, full: torch.Tensor, shard_rows: int, async_op: bool):
+        if self.layout.rows == 1 or self.P == 1:
+            return None
+        s1, s2, nslots, pmax = self.plan(shard_rows)
+        v1 = self._views(full, shard_rows, s1, nslots, pmax)
+        v2 = self._views(full, shard_rows, s2, nslots, pmax)
+        if self.backend != "nccl":
+            host = full.is_cuda
+            if host:
+                torch.cuda.current_stream(full.device).synchronize()
+            self._run_stage(v1, host)
+            self._run_stage(v2, host)
+            return None
+        main = torch.cuda.current_stream(full.device)
+        if self._stream is None:
+            self._stream = torch.cuda.Stream(device=full.device)
+        self._stream.wait_stream(main)
+        with torch.cuda.stream(self._stream):
+            self._run_stage(v1, False)  # wait(): the side stream waits for stage 1
+            self._run_stage(v2, False)
+            ev = torch.cuda.Event()
+            ev.record(self._stream)
+        done = _StreamDone(ev)
+        if not async_op:
+            done.wait()
+            return None
+        return done
+
+
 class NullComm:
     """No exchange (emulation of one rank on one GPU; the gathered rows keep stale data)."""
 
@@ -156,9 +316,11 @@ class PartitionedAPPNP:
     @classmethod
     def create(cls, indptr, indices, n, H, K, alpha, device, layout: Layout | None = None,
                overlap=False, data=None, mode="sym", comm=None, step_fn=None, graph_fn=None,
-               p_drop=0.0, seed=0, rank=None, world=None):
+               p_drop=0.0, seed=0, rank=None, world=None, exchange="multipath"):
         """rank / world override the process group's (single-GPU emulation of one rank of a
-        larger layout, with a ``NullComm``: measures that rank's kernel time only)."""
+        larger layout, with a ``NullComm``: measures that rank's kernel time only).
+        exchange: 'multipath' (MultipathComm, R x C layouts with C > 1) or 'group' (one RCCL
+        all-gather per column group); a pure row layout always uses the all-gather."""
         if rank is None:
             rank = dist.get_rank() if dist.is_initialized() else 0
         if world is None:
@@ -187,10 +349,17 @@ class PartitionedAPPNP:
         bufs = [torch.zeros(rows_pad, ld, dtype=H.dtype, device=device) for _ in range(2)]
         partial = (torch.zeros(max(hi - lo, 0), ld, dtype=torch.float32, device=device)
                    if overlap else None)
-        comm = comm or _TorchComm(layout, rank)
+        if comm is None:
+            if exchange not in ("multipath", "group"):
+                raise ValueError(f"unknown exchange {exchange!r}")
+            comm = (MultipathComm(layout, rank)
+                    if exchange == "multipath" and layout.rows > 1 and layout.cols > 1
+                    else _TorchComm(layout, rank))
         step_fn = step_fn or _hip_step
-        return cls(layout, rank, n, f, K, alpha, graph, H_slab, f_lo, f_hi, bufs, shard, lo, hi,
-                   comm, step_fn, overlap, partial, p_drop, seed)
+        obj = cls(layout, rank, n, f, K, alpha, graph, H_slab, f_lo, f_hi, bufs, shard, lo, hi,
+                  comm, step_fn, overlap, partial, p_drop, seed)
+        obj.exchange = "multipath" if isinstance(comm, MultipathComm) else "group"
+        return obj
 
     @property
     def nnz_hat_local(self) -> int:
@@ -260,6 +429,19 @@ def _hip_step(runner: PartitionedAPPNP, src, out_rows, k, part):
     else:
         step(runner.graph, Zin, H, out_rows[:, :w], k, runner.alpha, p_drop=runner.p_drop,
              seed=runner.seed)
+
+
+def candidate_layouts(world: int, f: int):
+    """(layout, overlap, exchange) variants ``bench.py --layout auto`` times after warm-up,
+    keeping the fastest (max over ranks).  The column partition needs no exchange; from 8 ranks
+    on, 2 row groups halve each rank's gathers for an exchange of half a slab per iteration,
+    which only an xGMI measurement can price."""
+    first = choose_layout(world, 0, f, 0)
+    cands = [(first, False, "group")]
+    if world >= 8 and world % 2 == 0 and f >= world // 2:
+        two = Layout(2, world // 2)
+        cands += [(two, True, "multipath"), (two, True, "group")]
+    return cands
 
 
 def choose_layout(world: int, n: int, f: int, nnz: int, elem_bytes: int = 4) -> Layout:

@@ -1,4 +1,4 @@
-"""CPU, world_size 2 (gloo): the multi-GPU orchestration of ppnp_amd.dist against the oracle.
+"""CPU, world_size 2-8 (gloo): the multi-GPU orchestration of ppnp_amd.dist against the oracle.
 
 The per-iteration kernel is replaced by an oracle step on the same CSR rows (the GPU kernel
 itself is covered by tests/test_gpu_parity.py); what is tested here is the layout, the row /
@@ -53,7 +53,7 @@ def _oracle_step(runner, src, out_rows, k, part):
         out_rows[:, :w] = torch.from_numpy(a * (g.rows_csr @ Zin) + runner.alpha * H).float()
 
 
-def _worker(rank, world, port, layout_spec, overlap, q):
+def _worker(rank, world, port, layout_spec, overlap, q, exchange="multipath"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -66,7 +66,8 @@ def _worker(rank, world, port, layout_spec, overlap, q):
         layout = Layout.parse(layout_spec, world)
         runner = PartitionedAPPNP.create(
             None, None, N, H, K, ALPHA, "cpu", layout=layout, overlap=overlap,
-            graph_fn=lambda lo, hi, ov: _FakeGraph(a_hat, lo, hi, ov), step_fn=_oracle_step)
+            graph_fn=lambda lo, hi, ov: _FakeGraph(a_hat, lo, hi, ov), step_fn=_oracle_step,
+            exchange=exchange)
         Z = runner.run()
         ref = O.appnp_propagate(a_hat, H.numpy(), K, ALPHA)
         sub = ref[runner.lo:runner.hi, runner.f_lo:runner.f_hi]
@@ -84,14 +85,18 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("layout,overlap", [("row", False), ("row", True), ("col", False),
-                                            ("1x2", False)])
-def test_partitioned_matches_oracle(layout, overlap):
-    world = 2
+@pytest.mark.parametrize("world,layout,overlap,exchange", [
+    (2, "row", False, "group"), (2, "row", True, "group"), (2, "col", False, "group"),
+    (2, "1x2", False, "group"),
+    # R x C layouts: two-stage relayed exchange over every rank (MultipathComm) and the
+    # plain column-group all-gather
+    (8, "2x4", True, "multipath"), (8, "2x4", False, "multipath"), (8, "4x2", True, "multipath"),
+    (4, "2x2", False, "multipath"), (8, "2x4", True, "group")])
+def test_partitioned_matches_oracle(world, layout, overlap, exchange):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    mp.start_processes(_worker, args=(world, _free_port(), layout, overlap, q), nprocs=world,
-                       join=True, start_method="spawn")
+    mp.start_processes(_worker, args=(world, _free_port(), layout, overlap, q, exchange),
+                       nprocs=world, join=True, start_method="spawn")
     res = sorted(q.get() for _ in range(world))
     covered = np.zeros((N, F), dtype=bool)
     for rank, lo, hi, flo, fhi, err in res:
@@ -117,3 +122,42 @@ def test_layout_helpers():
     assert line_ld(25) == 32 and line_ld(13) == 16 and line_ld(50) == 64 and line_ld(100) == 100
     assert line_ld(7) == 8 and line_ld(40, 2) == 64 and line_ld(100, 2) == 128
     assert choose_layout(8, 2_449_029, 100, 126_000_000) == Layout(1, 8)
+    from ppnp_amd.dist import candidate_layouts
+
+    assert candidate_layouts(2, 100) == [(Layout(1, 2), False, "group")]
+    c8 = candidate_layouts(8, 100)
+    assert c8[0] == (Layout(1, 8), False, "group") and (Layout(2, 4), True, "multipath") in c8
+
+
+@pytest.mark.parametrize("spec,world", [("2x4", 8), ("4x2", 8), ("2x2", 4), ("2x3", 6)])
+def test_multipath_plan(spec, world):
+    """Every send has a matching receive (same pair, origin, rows, in the same per-pair order),
+    each rank ends up with every row of its column group's shards, and the per-link load of a
+    stage is at most (R-1) pieces."""
+    from collections import Counter, defaultdict
+
+    from ppnp_amd.dist import Layout, MultipathComm
+
+    layout = Layout.parse(spec, world)
+    shard = 1000
+    plans = {r: MultipathComm(layout, r).plan(shard) for r in range(world)}
+    for stage in (0, 1):
+        sends, recvs = defaultdict(list), defaultdict(list)
+        load = Counter()
+        for r, p in plans.items():
+            for kind, peer, origin, rows, _ in p[stage]:
+                if kind == "send":
+                    sends[(r, peer)].append((origin, rows))
+                    load[(r, peer)] += rows[1] - rows[0]
+                else:
+                    recvs[(peer, r)].append((origin, rows))
+        assert sends == recvs
+        piece = -(-shard // (world - 1))
+        assert max(load.values()) <= (layout.rows - 1 if stage else 1) * piece
+    for r, p in plans.items():
+        got = defaultdict(int)
+        for kind, peer, origin, rows, where in p[0] + p[1]:
+            if kind == "recv" and where == "full":
+                got[origin] += rows[1] - rows[0]
+        group = MultipathComm(layout, r).group_of(r)
+        assert dict(got) == {a: shard for a in group if a != r}

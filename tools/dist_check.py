@@ -2,7 +2,8 @@
 """End-to-end check of the multi-GPU path on real HIP kernels.
 
     torchrun --nproc-per-node P --master-addr 127.0.0.1 tools/dist_check.py --layout row|col|RxC
-        [--overlap] [--n 60000] [--m 400000] [--f 20] [--K 10] [--p-drop 0.0]
+        [--overlap] [--exchange multipath|group] [--n 60000] [--m 400000] [--f 20] [--K 10]
+        [--p-drop 0.0]
 
 Every rank runs its share (ppnp_amd.dist.PartitionedAPPNP) and compares its block of Z_K with
 the single-GPU propagation of the whole graph computed on its own device.  Backend: RCCL when
@@ -25,6 +26,7 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--layout", default="col")
     p.add_argument("--overlap", action="store_true")
+    p.add_argument("--exchange", default="multipath", choices=["multipath", "group"])
     p.add_argument("--n", type=int, default=60000)
     p.add_argument("--m", type=int, default=400000)
     p.add_argument("--f", type=int, default=20)
@@ -52,7 +54,7 @@ def main():
     H = synth.features(a.n, a.f, device=dev, seed=1)
     runner = pdist.PartitionedAPPNP.create(indptr, indices, a.n, H, a.K, a.alpha, dev,
                                            layout=layout, overlap=a.overlap,
-                                           p_drop=a.p_drop, seed=5)
+                                           p_drop=a.p_drop, seed=5, exchange=a.exchange)
     Z = runner.run()
     torch.cuda.synchronize()
     G = ppnp_amd.Graph.from_csr(indptr, indices, None, a.n, device=dev)
@@ -62,7 +64,8 @@ def main():
     tol = 1e-5 * ref.abs().max().item() + 1e-6
     ok = err <= tol
     print(f"[dist_check] rank {rank}/{world} backend={dist.get_backend()} layout={layout} "
-          f"overlap={runner.overlap} rows [{runner.lo},{runner.hi}) cols [{runner.f_lo},"
+          f"overlap={runner.overlap} exchange={runner.exchange} rows [{runner.lo},{runner.hi}) "
+          f"cols [{runner.f_lo},"
           f"{runner.f_hi}) max err {err:.3e} tol {tol:.3e} -> {'OK' if ok else 'FAIL'}",
           flush=True)
     flag = torch.tensor([0 if ok else 1], dtype=torch.int64,
