@@ -205,8 +205,11 @@ def _splitmix64(x):
 
 
 def drop_threshold(p_drop: float) -> int:
-    """24-bit threshold: an edge is dropped when its 24-bit hash < threshold."""
-    return int(min(max(p_drop, 0.0), 1.0) * (1 << 24))
+    """24-bit threshold: an edge is dropped when its 24-bit hash < threshold.  p crosses the
+    C ABI as a float, so the threshold is taken from float32(p) (0.3 -> 5033165, where the
+    double 0.3 would give 5033164)."""
+    p = float(np.float32(min(max(p_drop, 0.0), 1.0)))
+    return int(p * (1 << 24))
 
 
 def edge_keep_mask(rows, cols, k: int, p_drop: float, seed: int):
@@ -229,7 +232,7 @@ def masked_operator(a_hat, k: int, p_drop: float, seed: int):
     n = a.shape[0]
     rows = np.repeat(np.arange(n, dtype=np.int64), np.diff(a.indptr))
     keep = edge_keep_mask(rows, a.indices, k, p_drop, seed)
-    scale = float(np.float32(1.0) / np.float32(1.0 - p_drop))
+    scale = float(np.float32(1.0) / (np.float32(1.0) - np.float32(p_drop)))
     data = np.where(keep, a.data * scale, 0.0)
     return sp.csr_matrix((data, a.indices, a.indptr), shape=a.shape)
 

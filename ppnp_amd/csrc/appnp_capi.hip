@@ -90,6 +90,7 @@ StepArgs base_args(const appnp_graph* g, int64_t f, float alpha) {
   a.col = g->col;
   a.val = g->val;
   a.n_rows = g->row_hi - g->row_lo;
+  a.nnz = g->nnz_hat;
   a.zin_rows = g->n;
   a.row_lo = g->row_lo;
   a.f = (int32_t)f;
@@ -350,6 +351,7 @@ int appnp_spmm(const int32_t* indptr, const int32_t* indices, const float* vals,
   a.out = Cm;
   a.ld_out = ld_c;
   a.n_rows = rows;
+  a.nnz = -1;  // not known on the host without a device read
   a.zin_rows = cols;
   a.row_lo = 0;
   a.f = (int32_t)f;
@@ -397,12 +399,14 @@ int appnp_step(const appnp_graph* g, int part, const void* Zin, int64_t ld_in, c
     a.n_hub = 0;
     if (part == APPNP_PART_LOCAL) {
       epi = appnp::EPI_PARTIAL;
+      a.nnz = g->nnz_local;
       a.row_ptr = g->lrow_ptr;
       a.col = g->lcol;
       a.val = g->lval;
     } else if (part == APPNP_PART_REMOTE) {
       if (!H || ld_h < f || !partial || ld_partial < f) return APPNP_EINVAL;
       epi = appnp::EPI_FINISH;
+      a.nnz = g->nnz_remote;
       a.row_ptr = g->rrow_ptr;
       a.col = g->rcol;
       a.val = g->rval;

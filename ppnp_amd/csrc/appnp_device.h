@@ -29,6 +29,7 @@ struct StepArgs {
   void* aux;               // BWD: dH (storage dtype); FINISH: fp32 partial
   int64_t ld_in, ld_h, ld_out, ld_aux;
   int64_t n_rows;          // rows held
+  int64_t nnz;             // entries of those rows (< 0: unknown); picks the row shape
   int64_t zin_rows;        // rows of zin (its last row is never over-read)
   int64_t row_lo;          // global index of local row 0 (hash key only)
   uint64_t mkey;           // per-iteration dropout key = splitmix64(seed + (k+1)*golden)
@@ -49,6 +50,7 @@ struct StepArgs {
 
 constexpr int kHeavyRow = 32;   // a row longer than this gets a whole wavefront (narrow)
 constexpr int kHubRow = 512;    // ... and one longer than this is dispatched first (wide)
+constexpr int kWideAvgRow = 24; // mean row length from which large graphs take a wave per row
 
 __host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
   x += 0x9E3779B97F4A7C15ull;

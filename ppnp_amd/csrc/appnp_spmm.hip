@@ -26,6 +26,11 @@
 
 namespace appnp {
 
+static int env_int(const char* name, int dflt) {
+  const char* s = getenv(name);
+  return (s && *s) ? atoi(s) : dflt;
+}
+
 namespace {
 
 // ---- row fragments: V consecutive elements at p.  With TAIL, a lane whose fragment crosses
@@ -385,11 +390,6 @@ int pick_vec(int dtype, int64_t f, const int64_t* lds, int n_ld, const void* con
   return v;
 }
 
-static int env_int(const char* name, int dflt) {
-  const char* s = getenv(name);
-  return (s && *s) ? atoi(s) : dflt;
-}
-
 hipError_t launch_step(int dtype, int epi, int V, const StepArgs& a_in, hipStream_t s) {
   StepArgs a = a_in;
   if (a.n_rows <= 0 || a.f <= 0) return hipSuccess;
@@ -414,7 +414,11 @@ hipError_t launch_step(int dtype, int epi, int V, const StepArgs& a_in, hipStrea
     V = v;
   }
   const int G = lanes_for(V);
-  const bool wide = G >= 16 || (latency && a.heavy && a.n_heavy > 0);
+  // Bandwidth regime: a wavefront per row also for narrow F once rows are long on average
+  // (products-synth slabs of 4-25 features, 51.5 entries a row: 6-10 % faster than G-lane
+  // rows; uniform and power-law; arxiv-synth, 14.8 a row: G-lane rows 20-50 % faster).
+  const bool long_rows = a.nnz >= (int64_t)kWideAvgRow * a.n_rows;
+  const bool wide = G >= 16 || (latency && a.heavy && a.n_heavy > 0) || (!latency && long_rows);
   const int64_t slabs = (a.f + (int64_t)G * V - 1) / ((int64_t)G * V);
   const int64_t rows_per_block = wide ? kWavesPerBlock : (int64_t)kWavesPerBlock * (kWave / G);
   // one wave per row (wide) by default: measured best on products-synth (tools/tune.sh)

@@ -669,3 +669,20 @@ def test_plan_replay_matches_propagate():
     torch.cuda.synchronize()
     assert torch.equal(plan().clone(), pa.propagate_forward(G, H, 10, 0.1))
     plan.close()
+
+
+@pytest.mark.parametrize("deg", [4, 14])
+@pytest.mark.parametrize("F", [3, 13, 25, 100])
+def test_bandwidth_regime_row_shapes(deg, F):
+    """Graphs above the latency regime (> 64k rows): mean row length < kWideAvgRow takes the
+    G-lane row kernel for narrow F, >= kWideAvgRow a wavefront per row (launch_step)."""
+    pa = _lib()
+    n = 70_000
+    adj = synth(n, deg * n, seed=deg + F)
+    G = pa.Graph.from_scipy(adj, device=DEV)
+    assert (G.nnz_hat >= 24 * n) == (deg == 14)
+    ah = O.calc_a_hat(adj, "sym")
+    H = torch.randn(n, F, generator=torch.Generator().manual_seed(F))
+    p = 0.3 if F == 13 else 0.0
+    Z = to_np(pa.propagate_forward(G, H.to(DEV), 4, 0.1, p_drop=p, seed=9))
+    close_fp32(Z, O.appnp_propagate(ah, H.numpy(), 4, 0.1, p_drop=p, seed=9))

@@ -144,3 +144,11 @@ def test_synth_graph_properties():
     assert a.diagonal().sum() == 0
     assert np.all(a.data == 1)
     assert a.has_sorted_indices
+
+
+def test_drop_threshold_follows_the_float_abi():
+    """p crosses the C ABI as a float: the oracle's threshold is float32(p) * 2^24 (0.3 ->
+    5033165, one more than the double 0.3 gives), matching set_drop in appnp_capi.hip."""
+    assert O.drop_threshold(0.3) == 5033165
+    assert O.drop_threshold(0.5) == 1 << 23
+    assert O.drop_threshold(0.0) == 0
