@@ -282,7 +282,7 @@ def main():
     parallelism = ((f"rows{runner.layout.rows}xcols{runner.layout.cols}"
                     + ("-overlap" if runner.overlap else "")
                     + (f"-{runner.exchange}" if runner.layout.rows > 1 and runner.layout.cols > 1
-                       else "")
+                       and runner.exchange != "none" else "")
                     + (f"-EMULATED-rank{args.emulate}" if args.emulate else ""))
                    if distributed else "single")
     traffic = committed_traffic(args.workload, dtype, parallelism)
@@ -298,8 +298,7 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "bf16" if dtype == torch.bfloat16 else "f32",
-        "data": "synthetic (uniform random graph with the dataset's node/edge counts, "
-                "H ~ N(0,1))",
+        "data": synth.DESCRIPTIONS.get(args.workload, "synthetic") + ", H ~ N(0,1)",
         "config": {
             "workload": args.workload,
             "nodes": n,

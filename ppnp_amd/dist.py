@@ -98,6 +98,8 @@ def line_ld(width: int, elem_bytes: int = 4) -> int:
 class _TorchComm:
     """In-place all-gather of equal row shards within a column group (RCCL for 'nccl')."""
 
+    name = "group"
+
     def __init__(self, layout: Layout, rank: int):
         self.layout = layout
         self.groups = {}
@@ -167,6 +169,8 @@ class MultipathComm:
     orders the caller's stream after the exchange.  On 'gloo' (CPU tests, single-GPU
     rehearsal) the exchange is synchronous and stages CUDA data through host memory.
     """
+
+    name = "multipath"
 
     def __init__(self, layout: Layout, rank: int):
         self.layout, self.rank = layout, rank
@@ -291,6 +295,8 @@ class MultipathComm:
 class NullComm:
     """No exchange (emulation of one rank on one GPU; the gathered rows keep stale data)."""
 
+    name = "none"
+
     def all_gather_rows(self, full, shard_rows, async_op):
         return None
 
@@ -358,7 +364,7 @@ class PartitionedAPPNP:
         step_fn = step_fn or _hip_step
         obj = cls(layout, rank, n, f, K, alpha, graph, H_slab, f_lo, f_hi, bufs, shard, lo, hi,
                   comm, step_fn, overlap, partial, p_drop, seed)
-        obj.exchange = "multipath" if isinstance(comm, MultipathComm) else "group"
+        obj.exchange = getattr(comm, "name", "group")
         return obj
 
     @property

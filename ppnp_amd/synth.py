@@ -28,6 +28,10 @@ CONFIGS = {
 SEEDS = {"pubmed-synth": 1, "ms-academic-synth": 2, "arxiv-synth": 3, "products-synth": 4,
          "products-powerlaw": 5}
 POWERLAW = {"products-powerlaw"}
+DESCRIPTIONS = {name: "synthetic (uniform random graph with the dataset's node/edge counts)"
+                for name in CONFIGS}
+DESCRIPTIONS["products-powerlaw"] = ("synthetic (Chung-Lu power-law graph with the dataset's "
+                                     "node/edge counts)")
 
 
 def uniform_graph_device(n: int, m: int, seed: int, device="cuda"):
