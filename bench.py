@@ -164,10 +164,13 @@ def main():
         P, r = (int(x) for x in args.emulate.split(":"))
         emu = dict(rank=r, world=P, comm=pdist.NullComm())
         lw = P
+    esz = 2 if dtype == torch.bfloat16 else 4
+    mem = torch.cuda.get_device_properties(dev).total_memory
+    nnz_bound = 2 * m + n  # nnz(A_hat) <= 2 m + n (symmetrised edges + diagonal)
     if args.layout == "auto" and world > 1 and not args.emulate:
-        cands = pdist.candidate_layouts(world, F)
+        cands = pdist.candidate_layouts(world, F, n, nnz_bound, esz, mem)
     else:
-        layout = (pdist.choose_layout(lw, n, F, m) if args.layout == "auto"
+        layout = (pdist.choose_layout(lw, n, F, nnz_bound, esz, mem) if args.layout == "auto"
                   else pdist.Layout.parse(args.layout, lw))
         cands = [(layout, args.overlap, args.exchange)]
     if world > 1:
@@ -184,7 +187,6 @@ def main():
     t0 = time.perf_counter()
     indptr, indices = synth.graph_for(args.workload, device=dev)
     H = synth.features(n, F, dtype=dtype, device=dev)
-    esz = 2 if dtype == torch.bfloat16 else 4
     ld = pdist.line_ld(F, esz)
     if ld != F:  # line-aligned rows; H/Z are [N, F] views of [N, ld] buffers
         Hbuf = torch.zeros(n, ld, dtype=dtype, device=dev)

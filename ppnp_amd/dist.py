@@ -437,23 +437,78 @@ def _hip_step(runner: PartitionedAPPNP, src, out_rows, k, part):
              seed=runner.seed)
 
 
-def candidate_layouts(world: int, f: int):
+INT32_MAX = 2**31 - 1
+
+
+def rank_bytes(layout: Layout, n: int, f: int, nnz_hat: int, elem_bytes: int = 4,
+               overlap: bool = False) -> int:
+    """Device bytes one rank of ``layout`` holds for the K loop (upper estimate): its rows'
+    CSR (int32 row_ptr, int32 col + fp32 val; doubled by the local/remote split of overlap
+    mode), dinv (fp64, all n), the H slab of its rows, two full-height Z slabs, and the fp32
+    partial of overlap mode."""
+    R, C = layout.rows, layout.cols
+    shard = -(-n // R)
+    nnz_r = -(-nnz_hat // R)
+    width = -(-f // C)
+    ld = line_ld(width, elem_bytes)
+    csr = 4 * (shard + 1) + 8 * nnz_r
+    if overlap:
+        csr += 4 * 2 * (shard + 1) + 8 * nnz_r
+    dense = (shard + 2 * shard * R) * ld * elem_bytes + (shard * ld * 4 if overlap else 0)
+    return csr + 8 * n + dense
+
+
+def fits(layout: Layout, n: int, f: int, nnz_hat: int, elem_bytes: int = 4,
+         overlap: bool = False, mem_bytes: int | None = None, headroom: float = 0.85) -> bool:
+    """Whether a rank's share stays inside the int32 CSR index range and, given the device
+    memory, inside ``headroom`` of it.  A feature-column layout replicates the whole CSR on
+    every rank; only row groups split it (the north_star's 'graphs that outgrow one GPU')."""
+    if -(-nnz_hat // layout.rows) > INT32_MAX:
+        return False
+    if mem_bytes is None:
+        return True
+    return rank_bytes(layout, n, f, nnz_hat, elem_bytes, overlap) <= headroom * mem_bytes
+
+
+def candidate_layouts(world: int, f: int, n: int = 0, nnz_hat: int = 0, elem_bytes: int = 4,
+                      mem_bytes: int | None = None):
     """(layout, overlap, exchange) variants ``bench.py --layout auto`` times after warm-up,
     keeping the fastest (max over ranks).  The column partition needs no exchange; from 8 ranks
     on, 2 row groups halve each rank's gathers for an exchange of half a slab per iteration,
-    which only an xGMI measurement can price."""
-    first = choose_layout(world, 0, f, 0)
+    which only an xGMI measurement can price.  Candidates that do not
+    fit (``fits``) are dropped; if none does, the row-heaviest layout that fits is used."""
+    first = choose_layout(world, n, f, nnz_hat, elem_bytes, mem_bytes)
+    if first.rows > 1:  # row groups forced by size: overlap the exchange, try both routes
+        return [(first, True, "multipath"), (first, True, "group")] if first.cols > 1 else [
+            (first, True, "group")]
     cands = [(first, False, "group")]
     if world >= 8 and world % 2 == 0 and f >= world // 2:
         two = Layout(2, world // 2)
-        cands += [(two, True, "multipath"), (two, True, "group")]
+        if fits(two, n, f, nnz_hat, elem_bytes, True, mem_bytes):
+            cands += [(two, True, "multipath"), (two, True, "group")]
     return cands
 
 
-def choose_layout(world: int, n: int, f: int, nnz: int, elem_bytes: int = 4) -> Layout:
+def choose_layout(world: int, n: int, f: int, nnz: int, elem_bytes: int = 4,
+                  mem_bytes: int | None = None) -> Layout:
     """Default layout: the column partition (no data-path collective) unless F is too narrow
-    to split; see DESIGN.md 'Multi-GPU' for the line-request model behind it."""
+    to split or a rank's share would not fit (``fits``): then the fewest row groups R (a
+    divisor of world) whose shares fit.  Row groups split the CSR, column groups split Z: a
+    row layout holds all n rows of Z, so the smallest share is usually a 2-D layout.  See DESIGN.md 'Multi-GPU' for the line-request model
+    behind the preference."""
     if f >= world:
-        return Layout(1, world)
-    c = max(1, math.gcd(world, f))
-    return Layout(world // c, c)
+        pref = Layout(1, world)
+    else:
+        c = max(1, math.gcd(world, f))
+        pref = Layout(world // c, c)
+    if fits(pref, n, f, nnz, elem_bytes, False, mem_bytes):
+        return pref
+    options = [Layout(r, world // r) for r in range(pref.rows + 1, world + 1) if world % r == 0]
+    for lay in options:
+        if fits(lay, n, f, nnz, elem_bytes, False, mem_bytes):
+            return lay
+    # nothing fits the memory: the smallest share inside the index range (the build then
+    # reports APPNP_ENOMEM if it really does not fit)
+    ok = [lay for lay in [pref] + options if fits(lay, n, f, nnz, elem_bytes)] or [
+        Layout(world, 1)]
+    return min(ok, key=lambda lay: rank_bytes(lay, n, f, nnz, elem_bytes))

@@ -129,6 +129,30 @@ def test_layout_helpers():
     assert c8[0] == (Layout(1, 8), False, "group") and (Layout(2, 4), True, "multipath") in c8
 
 
+def test_layout_memory_and_index_limits():
+    """Graphs that outgrow one GPU: a column layout replicates the CSR, so a graph whose CSR
+    does not fit a rank (or exceeds the int32 index range) gets row groups."""
+    from ppnp_amd.dist import Layout, candidate_layouts, choose_layout, fits, rank_bytes
+
+    gb = 1 << 30
+    # products-synth on 288 GB: column layout, 2x4 also a candidate
+    n, nnz = 2_449_029, 126_166_051
+    assert choose_layout(8, n, 100, nnz, 4, 288 * gb) == Layout(1, 8)
+    assert (Layout(2, 4), True, "multipath") in candidate_layouts(8, 100, n, nnz, 4, 288 * gb)
+    # papers100M-sized: 111 M nodes, 3.2 G nnz -- over int32 unless split in two row groups
+    n2, nnz2 = 111_059_956, 3_228_124_712
+    assert not fits(Layout(1, 8), n2, 128, nnz2)
+    assert choose_layout(8, n2, 128, nnz2, 4, 288 * gb) == Layout(2, 4)
+    assert candidate_layouts(8, 128, n2, nnz2, 4, 288 * gb) == [
+        (Layout(2, 4), True, "multipath"), (Layout(2, 4), True, "group")]
+    # row groups split the CSR, column groups split Z: 2x4 holds the smallest share here
+    shares = {lay: rank_bytes(lay, n, 100, nnz) for lay in
+              (Layout(1, 8), Layout(2, 4), Layout(4, 2), Layout(8, 1))}
+    assert min(shares, key=shares.get) == Layout(2, 4)
+    assert choose_layout(8, n, 100, nnz, 4, int(1.45 * gb)) == Layout(2, 4)
+    assert choose_layout(8, n, 100, nnz, 4, gb // 2) == Layout(2, 4)  # nothing fits: smallest
+
+
 @pytest.mark.parametrize("spec,world", [("2x4", 8), ("4x2", 8), ("2x2", 4), ("2x3", 6)])
 def test_multipath_plan(spec, world):
     """Every send has a matching receive (same pair, origin, rows, in the same per-pair order),
