@@ -24,6 +24,7 @@ Extra JSON fields:
 from __future__ import annotations
 
 import argparse
+import datetime
 import json
 import os
 import sys
@@ -179,7 +180,10 @@ def main():
         rows = any(c[0].rows > 1 for c in cands)
         backend = os.environ.get("PPNP_DIST_BACKEND") or ("nccl" if rows else "gloo")
         if backend == "nccl":
-            torch.distributed.init_process_group("nccl", device_id=dev)
+            # a collective that stalls aborts the job after 5 minutes (watchdog) instead of
+            # holding the node for the default 10
+            torch.distributed.init_process_group("nccl", device_id=dev,
+                                                 timeout=datetime.timedelta(minutes=5))
         else:
             torch.distributed.init_process_group(backend)
     ctl_dev = dev if world > 1 and torch.distributed.get_backend() == "nccl" else "cpu"
