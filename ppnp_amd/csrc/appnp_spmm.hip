@@ -324,50 +324,55 @@ __global__ __launch_bounds__(kBlock) void k_step_narrow(StepArgs a) {
   }
 }
 
-template <typename T, int V, int EPI, bool TAIL>
-hipError_t launch_g(int G, bool wide, dim3 grid, const StepArgs& a, hipStream_t s) {
-  // entries in flight per sub-group (wide): 1 -- occupancy supplies the memory-level
-  // parallelism; measured equal (products fp32) or faster (arxiv fp32 +3 %, bf16 +9-19 %)
-  // than 2, 4 or 8, which cost VGPRs
-  constexpr int UW = 1;
-  constexpr int UN = 4;  // entries in flight per row (narrow)
+template <typename T, int V, int EPI, bool TAIL, int U>
+hipError_t launch_wide(int G, dim3 grid, const StepArgs& a, hipStream_t s) {
   const dim3 block(kBlock);
-  if (wide && G < 16) {  // small graphs: a wavefront per row even for narrow rows
-    switch (G) {
-      case 1: hipLaunchKernelGGL((k_step_wide<T, V, 1, EPI, UW, TAIL>), grid, block, 0, s, a); break;
-      case 2: hipLaunchKernelGGL((k_step_wide<T, V, 2, EPI, UW, TAIL>), grid, block, 0, s, a); break;
-      case 4: hipLaunchKernelGGL((k_step_wide<T, V, 4, EPI, UW, TAIL>), grid, block, 0, s, a); break;
-      case 8: hipLaunchKernelGGL((k_step_wide<T, V, 8, EPI, UW, TAIL>), grid, block, 0, s, a); break;
-      default: return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
+  switch (G) {
+    case 1: hipLaunchKernelGGL((k_step_wide<T, V, 1, EPI, U, TAIL>), grid, block, 0, s, a); break;
+    case 2: hipLaunchKernelGGL((k_step_wide<T, V, 2, EPI, U, TAIL>), grid, block, 0, s, a); break;
+    case 4: hipLaunchKernelGGL((k_step_wide<T, V, 4, EPI, U, TAIL>), grid, block, 0, s, a); break;
+    case 8: hipLaunchKernelGGL((k_step_wide<T, V, 8, EPI, U, TAIL>), grid, block, 0, s, a); break;
+    case 16: hipLaunchKernelGGL((k_step_wide<T, V, 16, EPI, U, TAIL>), grid, block, 0, s, a); break;
+    case 32: hipLaunchKernelGGL((k_step_wide<T, V, 32, EPI, U, TAIL>), grid, block, 0, s, a); break;
+    case 64: hipLaunchKernelGGL((k_step_wide<T, V, 64, EPI, U, TAIL>), grid, block, 0, s, a); break;
+    default: return hipErrorInvalidValue;
   }
+  return hipGetLastError();
+}
+
+template <typename T, int V, int EPI, bool TAIL>
+hipError_t launch_g(int G, bool wide, int uw, dim3 grid, const StepArgs& a, hipStream_t s) {
+  constexpr int UN = 4;  // entries in flight per row (narrow)
+  if (wide) {
+    if (uw == 8) return launch_wide<T, V, EPI, TAIL, 8>(G, grid, a, s);
+    if (uw == 4) return launch_wide<T, V, EPI, TAIL, 4>(G, grid, a, s);
+    return launch_wide<T, V, EPI, TAIL, 1>(G, grid, a, s);
+  }
+  const dim3 block(kBlock);
   switch (G) {
     case 1: hipLaunchKernelGGL((k_step_narrow<T, V, 1, EPI, UN, TAIL>), grid, block, 0, s, a); break;
     case 2: hipLaunchKernelGGL((k_step_narrow<T, V, 2, EPI, UN, TAIL>), grid, block, 0, s, a); break;
     case 4: hipLaunchKernelGGL((k_step_narrow<T, V, 4, EPI, UN, TAIL>), grid, block, 0, s, a); break;
     case 8: hipLaunchKernelGGL((k_step_narrow<T, V, 8, EPI, UN, TAIL>), grid, block, 0, s, a); break;
-    case 16: hipLaunchKernelGGL((k_step_wide<T, V, 16, EPI, UW, TAIL>), grid, block, 0, s, a); break;
-    case 32: hipLaunchKernelGGL((k_step_wide<T, V, 32, EPI, UW, TAIL>), grid, block, 0, s, a); break;
-    case 64: hipLaunchKernelGGL((k_step_wide<T, V, 64, EPI, UW, TAIL>), grid, block, 0, s, a); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
 
 template <typename T, int EPI>
-hipError_t launch_v(int V, int G, bool wide, dim3 grid, const StepArgs& a, hipStream_t s) {
+hipError_t launch_v(int V, int G, bool wide, int uw, dim3 grid, const StepArgs& a,
+                    hipStream_t s) {
   const bool tail = (a.f % V) != 0;
   switch (V) {
-    case 1: return launch_g<T, 1, EPI, false>(G, wide, grid, a, s);
-    case 2: return tail ? launch_g<T, 2, EPI, true>(G, wide, grid, a, s)
-                        : launch_g<T, 2, EPI, false>(G, wide, grid, a, s);
-    case 4: return tail ? launch_g<T, 4, EPI, true>(G, wide, grid, a, s)
-                        : launch_g<T, 4, EPI, false>(G, wide, grid, a, s);
+    case 1: return launch_g<T, 1, EPI, false>(G, wide, uw, grid, a, s);
+    case 2: return tail ? launch_g<T, 2, EPI, true>(G, wide, uw, grid, a, s)
+                        : launch_g<T, 2, EPI, false>(G, wide, uw, grid, a, s);
+    case 4: return tail ? launch_g<T, 4, EPI, true>(G, wide, uw, grid, a, s)
+                        : launch_g<T, 4, EPI, false>(G, wide, uw, grid, a, s);
     case 8:
       if constexpr (sizeof(T) == 2)
-        return tail ? launch_g<T, 8, EPI, true>(G, wide, grid, a, s)
-                    : launch_g<T, 8, EPI, false>(G, wide, grid, a, s);
+        return tail ? launch_g<T, 8, EPI, true>(G, wide, uw, grid, a, s)
+                    : launch_g<T, 8, EPI, false>(G, wide, uw, grid, a, s);
       return hipErrorInvalidValue;
     default: return hipErrorInvalidValue;
   }
@@ -421,7 +426,8 @@ hipError_t launch_step(int dtype, int epi, int V, const StepArgs& a_in, hipStrea
   // (products-synth slabs of 4-25 features, 51.5 entries a row: 6-10 % faster than G-lane
   // rows; uniform and power-law; arxiv-synth, 14.8 a row: G-lane rows 20-50 % faster).
   const bool long_rows = a.nnz >= (int64_t)kWideAvgRow * a.n_rows;
-  const bool wide = G >= 16 || (latency && a.heavy && a.n_heavy > 0) || (!latency && long_rows);
+  const bool heavy_rows = a.heavy && a.n_heavy > 0;
+  const bool wide = G >= 16 || (latency && heavy_rows) || (!latency && long_rows);
   const int64_t slabs = (a.f + (int64_t)G * V - 1) / ((int64_t)G * V);
   const int64_t rows_per_block = wide ? kWavesPerBlock : (int64_t)kWavesPerBlock * (kWave / G);
   // one wave per row (wide) by default: measured best on products-synth (tools/tune.sh)
@@ -443,17 +449,24 @@ hipError_t launch_step(int dtype, int epi, int V, const StepArgs& a_in, hipStrea
     a.n_heavy = 0;
   }
   const dim3 grid((unsigned)blocks, (unsigned)slabs);
+  // entries in flight per sub-group of the wide kernel.  Bandwidth regime: 1 -- occupancy
+  // supplies the memory-level parallelism; measured equal (products fp32) or faster (arxiv
+  // fp32 +3 %, bf16 +9-19 %) than 2, 4 or 8, which cost VGPRs.  Small graphs with long rows
+  // (latency regime, wave per row because of them): 8, so the longest row -- which sets the
+  // launch time -- takes few dependent rounds (Cora-ML 9.4 -> 5.8 us, Citeseer 5.4 -> 3.9 us
+  // per iteration; tools/sweep_uw_latency.sh).
+  const int uw = (latency && heavy_rows) ? 8 : 1;
   if (dtype == 0) {
     switch (epi) {
-      case EPI_FWD: return launch_v<float, EPI_FWD>(V, G, wide, grid, a, s);
-      case EPI_BWD: return launch_v<float, EPI_BWD>(V, G, wide, grid, a, s);
-      case EPI_PARTIAL: return launch_v<float, EPI_PARTIAL>(V, G, wide, grid, a, s);
-      case EPI_FINISH: return launch_v<float, EPI_FINISH>(V, G, wide, grid, a, s);
+      case EPI_FWD: return launch_v<float, EPI_FWD>(V, G, wide, uw, grid, a, s);
+      case EPI_BWD: return launch_v<float, EPI_BWD>(V, G, wide, uw, grid, a, s);
+      case EPI_PARTIAL: return launch_v<float, EPI_PARTIAL>(V, G, wide, uw, grid, a, s);
+      case EPI_FINISH: return launch_v<float, EPI_FINISH>(V, G, wide, uw, grid, a, s);
     }
   } else {
     switch (epi) {
-      case EPI_FWD: return launch_v<uint16_t, EPI_FWD>(V, G, wide, grid, a, s);
-      case EPI_BWD: return launch_v<uint16_t, EPI_BWD>(V, G, wide, grid, a, s);
+      case EPI_FWD: return launch_v<uint16_t, EPI_FWD>(V, G, wide, uw, grid, a, s);
+      case EPI_BWD: return launch_v<uint16_t, EPI_BWD>(V, G, wide, uw, grid, a, s);
     }
   }
   return hipErrorInvalidValue;

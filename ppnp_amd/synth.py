@@ -23,7 +23,12 @@ CONFIGS = {
     "products-synth": (2449029, 61859140, 100, 10, 0.1, torch.float32),
     # power-law stand-in (SURVEY 8(d) "optionally add a Chung-Lu power-law variant")
     "products-powerlaw": (2449029, 61859140, 100, 10, 0.1, torch.float32),
+    # the reference's own datasets (standardized LCC adjacency from tests/golden, which
+    # tests/golden/make_golden.py took from the reference's SparseGraph.standardize)
+    "cora-ml-real": (2810, 7981, 7, 10, 0.1, torch.float32),
+    "citeseer-real": (2110, 3668, 6, 10, 0.1, torch.float32),
 }
+REAL = {"cora-ml-real": "cora_ml", "citeseer-real": "citeseer"}
 
 SEEDS = {"pubmed-synth": 1, "ms-academic-synth": 2, "arxiv-synth": 3, "products-synth": 4,
          "products-powerlaw": 5}
@@ -32,6 +37,8 @@ DESCRIPTIONS = {name: "synthetic (uniform random graph with the dataset's node/e
                 for name in CONFIGS}
 DESCRIPTIONS["products-powerlaw"] = ("synthetic (Chung-Lu power-law graph with the dataset's "
                                      "node/edge counts)")
+for _name in REAL:
+    DESCRIPTIONS[_name] = "the reference's dataset (standardized LCC adjacency)"
 
 
 def uniform_graph_device(n: int, m: int, seed: int, device="cuda"):
@@ -84,7 +91,22 @@ def chung_lu_graph_device(n: int, m: int, seed: int, exponent: float = 3.2,
     return indptr.to(torch.int32), col
 
 
+def real_graph(name: str, device="cuda"):
+    """CSR of a dataset the reference ships, standardized as its SparseGraph does."""
+    import os
+
+    import numpy as np
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    d = np.load(os.path.join(root, "tests", "golden", name + ".npz"), allow_pickle=False)
+    indptr = torch.from_numpy(d["adj_indptr"].astype(np.int32)).to(device)
+    indices = torch.from_numpy(d["adj_indices"].astype(np.int32)).to(device)
+    return indptr, indices
+
+
 def graph_for(workload: str, device="cuda"):
+    if workload in REAL:
+        return real_graph(REAL[workload], device=device)
     n, m = CONFIGS[workload][:2]
     if workload in POWERLAW:
         return chung_lu_graph_device(n, m, SEEDS[workload], device=device)
