@@ -132,6 +132,8 @@ class APPNP(nn.Module):
         self.edge_drop = float(edge_drop)
         self.prop_dtype = dtype
         self._graph = None
+        self._memo = None  # (key, Z_K) of the last no-grad eval-mode propagation
+        self.memo_hits = 0
 
     def graph(self) -> Graph:
         dev = self.adj_indptr.device
@@ -150,10 +152,28 @@ class APPNP(nn.Module):
         Hc = H.to(self.prop_dtype)
         return propagate(self.graph(), Hc, self.K, self.alpha, p, seed).to(H.dtype)
 
+    def _memo_key(self, X):
+        """Identity of everything Z_K depends on, for deterministic (eval, no-grad) calls:
+        main.py evaluates the stopping and validation sets with two forwards of the same X
+        and weights (main.py:138, 145); the second reuses the first's Z_K.  Any in-place
+        change (optimizer step, load_state_dict, edited X) bumps a tensor version."""
+        if self.training or torch.is_grad_enabled():
+            return None
+        xs = (X.indptr, X.indices, X.data) if isinstance(X, SparseFeatures) else (X,)
+        state = [*xs, *self.parameters(), *self.buffers()]
+        return (tuple((t.data_ptr(), t._version, tuple(t.shape)) for t in state),
+                self.K, self.alpha, self.mode, self.prop_dtype)
+
     def forward(self, X, idx=None, ppr=None):
         """X: dense tensor (as the reference) or ppnp_amd.SparseFeatures (CSR on the GPU)."""
         if idx is not None:
-            return self.propagate(_encode(self.encoder, X, self.training))[idx]
+            key = self._memo_key(X)
+            if key is not None and self._memo is not None and self._memo[0] == key:
+                self.memo_hits += 1
+                return self._memo[1][idx]
+            Z = self.propagate(_encode(self.encoder, X, self.training))
+            self._memo = (key, Z) if key is not None else None
+            return Z[idx]
         elif ppr is not None:
             return ppr @ _encode(self.encoder, X, self.training)
         else:

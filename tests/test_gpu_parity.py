@@ -325,6 +325,36 @@ def test_ppnp_and_appnp_logits(ds, request):
     assert np.abs(out3 - ref3).max() <= 1e-4 * np.abs(ref3).max()
 
 
+def test_appnp_eval_memo(cora):
+    """Eval-mode, no-grad forwards of the same X and weights share one propagation (main.py
+    evaluates stopping and validation sets back to back); any change recomputes."""
+    pa = _lib()
+    g = cora
+    X = torch.from_numpy(g["ppnp_X"]).to(DEV)
+    idx = torch.from_numpy(g["ppnp_idx"]).to(DEV)
+    ap = pa.APPNP(n_features=X.shape[1], n_classes=int(g["n_classes"]), adj=adj_of(g)).to(DEV)
+    ap.eval()
+    with torch.no_grad():
+        a = ap(X, idx)
+        b = ap(X, idx[:7])
+        assert ap.memo_hits == 1 and torch.equal(a[:7], b)
+    opt = torch.optim.SGD(ap.parameters(), lr=0.1)
+    ap.train()
+    loss = ap(X, idx).square().sum()  # train mode: no memo, dropout active
+    opt.zero_grad()
+    loss.backward()
+    opt.step()  # weights change in place
+    ap.eval()
+    with torch.no_grad():
+        c = ap(X, idx)
+        assert ap.memo_hits == 1 and not torch.equal(a, c)
+        X.mul_(2.0)  # an in-place edit of X is seen too
+        d = ap(X, idx)
+        assert ap.memo_hits == 1 and not torch.equal(c, d)
+    e = ap(X, idx)  # grad enabled: never memoised
+    assert ap.memo_hits == 1 and torch.allclose(d, e)
+
+
 # ---------------------------------------------------------------------------------------
 # row-partitioned step (multi-GPU building block): held rows, local/remote split
 # ---------------------------------------------------------------------------------------
