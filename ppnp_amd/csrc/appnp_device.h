@@ -46,6 +46,9 @@ struct StepArgs {
   int64_t light_blocks;    // set by launch_step: blocks [light_blocks, grid) take heavy rows
   const int32_t* hub;      // rows longer than kHubRow: the wide kernels dispatch them first
   int64_t n_hub;
+  int32_t nt;              // cache policy of the streams (set by launch_step): bit 0 col/val,
+                           // bit 1 H, bit 2 Zout -- non-temporal, so they do not evict the
+                           // gathered rows of Zin from the Infinity Cache
 };
 
 constexpr int kHeavyRow = 32;   // a row longer than this gets a whole wavefront (narrow)
@@ -85,6 +88,21 @@ __device__ __forceinline__ uint32_t f32_to_bf16(float f) {
 template <typename T, int V>
 struct Io;
 
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+// non-temporal accesses for the streams (touched once per launch)
+template <typename W>
+__device__ __forceinline__ W ld_nt(const void* p) {
+  return __builtin_nontemporal_load(reinterpret_cast<const W*>(p));
+}
+template <typename W>
+__device__ __forceinline__ void st_nt(void* p, W w) {
+  __builtin_nontemporal_store(w, reinterpret_cast<W*>(p));
+}
+
 template <int V>
 struct Io<float, V> {
   static __device__ __forceinline__ void load(const float* p, float (&x)[V]) {
@@ -105,6 +123,26 @@ struct Io<float, V> {
       *reinterpret_cast<float2*>(p) = make_float2(x[0], x[1]);
     } else {
       *p = x[0];
+    }
+  }
+  static __device__ __forceinline__ void load_nt(const float* p, float (&x)[V]) {
+    if constexpr (V == 4) {
+      const f32x4 t = ld_nt<f32x4>(p);
+      x[0] = t.x; x[1] = t.y; x[2] = t.z; x[3] = t.w;
+    } else if constexpr (V == 2) {
+      const f32x2 t = ld_nt<f32x2>(p);
+      x[0] = t.x; x[1] = t.y;
+    } else {
+      x[0] = ld_nt<float>(p);
+    }
+  }
+  static __device__ __forceinline__ void store_nt(float* p, const float (&x)[V]) {
+    if constexpr (V == 4) {
+      st_nt<f32x4>(p, f32x4{x[0], x[1], x[2], x[3]});
+    } else if constexpr (V == 2) {
+      st_nt<f32x2>(p, f32x2{x[0], x[1]});
+    } else {
+      st_nt<float>(p, x[0]);
     }
   }
 };
@@ -148,6 +186,36 @@ struct Io<uint16_t, V> {  // bf16 storage
       *reinterpret_cast<uint32_t*>(p) = f32_to_bf16(x[0]) | (f32_to_bf16(x[1]) << 16);
     } else {
       *p = (uint16_t)f32_to_bf16(x[0]);
+    }
+  }
+  static __device__ __forceinline__ void load_nt(const uint16_t* p, float (&x)[V]) {
+    if constexpr (V == 8) {
+      const u32x4 t = ld_nt<u32x4>(p);
+      const uint32_t w[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        x[2 * i] = __uint_as_float(w[i] << 16);
+        x[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+      }
+    } else if constexpr (V == 4) {
+      const u32x2 t = ld_nt<u32x2>(p);
+      x[0] = __uint_as_float(t.x << 16); x[1] = __uint_as_float(t.x & 0xffff0000u);
+      x[2] = __uint_as_float(t.y << 16); x[3] = __uint_as_float(t.y & 0xffff0000u);
+    } else {
+      load(p, x);
+    }
+  }
+  static __device__ __forceinline__ void store_nt(uint16_t* p, const float (&x)[V]) {
+    if constexpr (V == 8) {
+      st_nt<u32x4>(p, u32x4{f32_to_bf16(x[0]) | (f32_to_bf16(x[1]) << 16),
+                            f32_to_bf16(x[2]) | (f32_to_bf16(x[3]) << 16),
+                            f32_to_bf16(x[4]) | (f32_to_bf16(x[5]) << 16),
+                            f32_to_bf16(x[6]) | (f32_to_bf16(x[7]) << 16)});
+    } else if constexpr (V == 4) {
+      st_nt<u32x2>(p, u32x2{f32_to_bf16(x[0]) | (f32_to_bf16(x[1]) << 16),
+                            f32_to_bf16(x[2]) | (f32_to_bf16(x[3]) << 16)});
+    } else {
+      store(p, x);
     }
   }
 };

@@ -58,9 +58,13 @@ __device__ __forceinline__ void st_at(T* p, const float (&x)[V]) {
 }
 
 template <typename T, int V, bool TAIL>
-__device__ __forceinline__ void frag_load(const T* p, float (&x)[V], int rem, bool full_ok) {
+__device__ __forceinline__ void frag_load(const T* p, float (&x)[V], int rem, bool full_ok,
+                                          bool nt = false) {
   if (!TAIL || rem >= V || full_ok) {
-    Io<T, V>::load(p, x);
+    if (nt)
+      Io<T, V>::load_nt(p, x);
+    else
+      Io<T, V>::load(p, x);
     return;
   }
 #pragma unroll
@@ -89,9 +93,12 @@ __device__ __forceinline__ void frag_load(const T* p, float (&x)[V], int rem, bo
 }
 
 template <typename T, int V, bool TAIL>
-__device__ __forceinline__ void frag_store(T* p, const float (&x)[V], int rem) {
+__device__ __forceinline__ void frag_store(T* p, const float (&x)[V], int rem, bool nt = false) {
   if (!TAIL || rem >= V) {
-    Io<T, V>::store(p, x);
+    if (nt)
+      Io<T, V>::store_nt(p, x);
+    else
+      Io<T, V>::store(p, x);
     return;
   }
   if constexpr (V == 8) {
@@ -127,7 +134,8 @@ __device__ __forceinline__ void epilogue(const StepArgs& a, int64_t row, int col
   if constexpr (EPI == EPI_FWD) {
 #pragma unroll
     for (int v = 0; v < V; ++v) y[v] = fmaf(a.alpha, hv[v], y[v]);
-    frag_store<T, V, TAIL>(static_cast<T*>(a.out) + row * a.ld_out + col0, y, rem);
+    frag_store<T, V, TAIL>(static_cast<T*>(a.out) + row * a.ld_out + col0, y, rem,
+                           a.nt & 4);
   } else if constexpr (EPI == EPI_BWD) {
     if (a.out) frag_store<T, V, TAIL>(static_cast<T*>(a.out) + row * a.ld_out + col0, y, rem);
     T* d = static_cast<T*>(a.aux) + row * a.ld_aux + col0;
@@ -153,7 +161,7 @@ __device__ __forceinline__ void load_h(const StepArgs& a, int64_t row, int col0,
                                        int rem) {
   if constexpr (EPI == EPI_FWD || EPI == EPI_FINISH) {
     frag_load<T, V, TAIL>(static_cast<const T*>(a.h) + row * a.ld_h + col0, hv, rem,
-                          row + 1 < a.n_rows);
+                          row + 1 < a.n_rows, a.nt & 2);
   } else {
 #pragma unroll
     for (int v = 0; v < V; ++v) hv[v] = 0.0f;
@@ -183,8 +191,15 @@ __device__ __forceinline__ void wave_row(const StepArgs& a, int64_t row, int lan
     int c = 0;
     float w = 0.0f;
     if (lane < n) {
-      c = a.col[cb + lane];
-      w = edge_weight(a.val ? a.val[cb + lane] : 1.0f, a.row_lo + row, c, a);
+      float v = 1.0f;
+      if (a.nt & 1) {
+        c = ld_nt<int32_t>(a.col + cb + lane);
+        if (a.val) v = ld_nt<float>(a.val + cb + lane);
+      } else {
+        c = a.col[cb + lane];
+        if (a.val) v = a.val[cb + lane];
+      }
+      w = edge_weight(v, a.row_lo + row, c, a);
     }
     tile[lane] = make_int2(c, __float_as_int(w));
     __builtin_amdgcn_wave_barrier();
@@ -297,8 +312,15 @@ __global__ __launch_bounds__(kBlock) void k_step_narrow(StepArgs a) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if (e + u < end) {
-          c[u] = a.col[e + u];
-          w[u] = edge_weight(a.val ? a.val[e + u] : 1.0f, a.row_lo + row, c[u], a);
+          float v = 1.0f;
+          if (a.nt & 1) {
+            c[u] = ld_nt<int32_t>(a.col + e + u);
+            if (a.val) v = ld_nt<float>(a.val + e + u);
+          } else {
+            c[u] = a.col[e + u];
+            if (a.val) v = a.val[e + u];
+          }
+          w[u] = edge_weight(v, a.row_lo + row, c[u], a);
         } else {
           c[u] = 0;
           w[u] = 0.0f;
@@ -421,13 +443,17 @@ hipError_t launch_step(int dtype, int epi, int V, const StepArgs& a_in, hipStrea
     while (v < V && (int64_t)64 * v < a.f) v <<= 1;
     V = v;
   }
+  static const int v_env = env_int("APPNP_VEC", -1);  // measurement override (<= pick_vec's)
+  if (v_env > 0 && v_env <= V) V = v_env;
   const int G = lanes_for(V);
   // Bandwidth regime: a wavefront per row also for narrow F once rows are long on average
   // (products-synth slabs of 4-25 features, 51.5 entries a row: 6-10 % faster than G-lane
   // rows; uniform and power-law; arxiv-synth, 14.8 a row: G-lane rows 20-50 % faster).
   const bool long_rows = a.nnz >= (int64_t)kWideAvgRow * a.n_rows;
   const bool heavy_rows = a.heavy && a.n_heavy > 0;
-  const bool wide = G >= 16 || (latency && heavy_rows) || (!latency && long_rows);
+  static const int wide_env = env_int("APPNP_WIDE", -1);  // measurement override
+  const bool wide = wide_env >= 0 ? wide_env != 0
+                                  : (G >= 16 || (latency && heavy_rows) || (!latency && long_rows));
   const int64_t slabs = (a.f + (int64_t)G * V - 1) / ((int64_t)G * V);
   const int64_t rows_per_block = wide ? kWavesPerBlock : (int64_t)kWavesPerBlock * (kWave / G);
   // one wave per row (wide) by default: measured best on products-synth (tools/tune.sh)
@@ -455,7 +481,11 @@ hipError_t launch_step(int dtype, int epi, int V, const StepArgs& a_in, hipStrea
   // (latency regime, wave per row because of them): 8, so the longest row -- which sets the
   // launch time -- takes few dependent rounds (Cora-ML 9.4 -> 5.8 us, Citeseer 5.4 -> 3.9 us
   // per iteration; tools/sweep_uw_latency.sh).
-  const int uw = (latency && heavy_rows) ? 8 : 1;
+  static const int uw_env = env_int("APPNP_UW", -1);  // measurement override (1, 4, 8)
+  const int uw = uw_env > 0 ? uw_env : (latency && heavy_rows) ? 8 : 1;
+  // cache policy of the streams (StepArgs::nt); APPNP_NT overrides for measurement
+  static const int nt_env = env_int("APPNP_NT", -1);
+  a.nt = nt_env >= 0 ? nt_env : (latency ? 0 : 1);
   if (dtype == 0) {
     switch (epi) {
       case EPI_FWD: return launch_v<float, EPI_FWD>(V, G, wide, uw, grid, a, s);
