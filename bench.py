@@ -50,6 +50,8 @@ def parse():
     p.add_argument("--workload", default="products-synth")
     p.add_argument("--dtype", default=None, choices=["f32", "bf16"],
                    help="override the workload's storage dtype (non-headline variants)")
+    p.add_argument("--features", type=int, default=None,
+                   help="override the workload's feature width F (non-headline variants)")
     p.add_argument("--cpu-iters", type=int, default=10,
                    help="iterations of the CPU baseline sample (0 disables it)")
     p.add_argument("--layout", default="auto",
@@ -157,6 +159,8 @@ def main():
     n, m, F, K, alpha, dtype = synth.CONFIGS[args.workload]
     if args.dtype:
         dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    if args.features:
+        F = args.features
     seed = synth.SEEDS.get(args.workload, 0)
     distributed = world > 1 or args.layout != "auto"
     emu = {}
@@ -279,9 +283,13 @@ def main():
     b_iter = 4 * (rows_local + 1) + 8 * nnz_local + 3 * rows_local * F_local * s
     avg_launch_ms = dev_ms / (args.steps * K)
     achieved = b_iter / (avg_launch_ms * 1e-3) / 1e9
-    # gather line-request rate: every nonzero gathers one row of Z_k
+    # gather line-request rate: every nonzero gathers one row of Z_k; with
+    # split rows only the fs main columns are gathered (whole lines), the rest run the
+    # L2-blocked remainder pass (appnp_blocks.hip)
+    fs = graph.split_point(F_local, dtype) if not distributed and K >= 2 else 0
     ld_l = pdist.line_ld(F_local, s)
-    lines_per_row = 1 if ld_l * s <= 128 else -(-(F_local * s) // 128)
+    lines_per_row = (fs * s // 128 if fs else
+                     1 if ld_l * s <= 128 else -(-(F_local * s) // 128))
     lines = nnz_local * lines_per_row + (8 * nnz_local + 3 * rows_local * ld_l * s) / 128
     line_rate = lines / (avg_launch_ms * 1e-3) / 1e9
     value = n * F * K * args.steps / wall
@@ -336,7 +344,9 @@ def main():
                 "frac": line_rate / GATHER_LINE_CEILING,
                 "ceiling_source": "tools/gather_probe.hip, profiles/r1_gather_probe.txt",
             },
-            "kernel": "k_step_wide (one launch per iteration)",
+            "kernel": ("k_step_wide (one launch per iteration)" if not fs else
+                       f"k_step_wide on columns [0, {fs}) + k_rem_block x {-(-n // (1 << 17))} "
+                       f"(remainder columns, L2-blocked) per iteration; times are per iteration"),
             "bytes_per_launch": b_iter,
             "avg_launch_ms": avg_launch_ms,
         },

@@ -59,6 +59,13 @@ enum appnp_norm { APPNP_NORM_SYM = 0, APPNP_NORM_RW = 1 };
  * for 'sym' on an undirected graph, where A_hat^T == A_hat. */
 #define APPNP_GRAPH_TRANSPOSE 0x100
 
+/* OR into `mode`: also keep a copy of A_hat blocked by source rows (2^17 per block; full
+ * graphs only).  appnp_propagate then takes the last 1-4 columns of fp32 rows with
+ * F = 32q + r (e.g. F = 100) out of the random gather and forms their product in an
+ * L2-resident pass, so a gathered row costs q cache lines instead of q + 1.  Costs one more
+ * copy of col/val plus (n/2^17 + 1) * n int32 offsets of device memory. */
+#define APPNP_GRAPH_SOURCE_BLOCKS 0x200
+
 /* storage type of H / Z (accumulation is always fp32) */
 enum appnp_dtype { APPNP_F32 = 0, APPNP_BF16 = 1 };
 
@@ -152,6 +159,13 @@ int appnp_graph_dinv(const appnp_graph* g, const double** dinv);
  * workspace holds the ping-pong iterates with its own line-aligned leading dimension
  * (`ld` is accepted for ABI stability and ignored). */
 size_t appnp_workspace_bytes(const appnp_graph* g, int64_t f, int64_t ld, int dtype);
+
+/* The column split appnp_propagate uses for this shape when H, Z and the workspace are 16-B
+ * aligned with leading dimensions that are multiples of 4 (K >= 2): *fs = 32q for fp32 rows of
+ * F = 32q + r features, 1 <= r <= 4, on a graph built with APPNP_GRAPH_SOURCE_BLOCKS (then
+ * columns [0, fs) gather whole cache lines and [fs, F) run the L2-blocked remainder pass);
+ * *fs = 0 when rows are gathered whole.  Informational: appnp_propagate decides by itself. */
+int appnp_propagate_split_point(const appnp_graph* g, int64_t f, int dtype, int64_t* fs);
 
 /*
  * Z = APPNP_K(H):  Z_0 = H;  Z_{k+1} = (1-alpha) (M_k o A_hat) Z_k + alpha H,  k < K.

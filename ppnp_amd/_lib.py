@@ -25,6 +25,7 @@ APPNP_ENOTSUP = -95
 
 NORM = {"sym": 0, "rw": 1}
 GRAPH_TRANSPOSE = 0x100
+GRAPH_SOURCE_BLOCKS = 0x200
 F32, BF16 = 0, 1
 PART_ALL, PART_LOCAL, PART_REMOTE = 0, 1, 2
 
@@ -48,6 +49,7 @@ _SIGS = {
     "appnp_graph_copy_csr": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp]),
     "appnp_graph_dinv": (_i32, [_vp, C.POINTER(_vp)]),
     "appnp_workspace_bytes": (_sz, [_vp, _i64, _i64, _i32]),
+    "appnp_propagate_split_point": (_i32, [_vp, _i64, _i32, C.POINTER(_i64)]),
     "appnp_propagate": (
         _i32,
         [_vp, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _f32, _f32, _u64, _vp, _sz, _vp],

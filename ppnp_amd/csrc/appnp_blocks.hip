@@ -1,0 +1,266 @@
+// appnp_blocks.hip -- remainder columns of a row through an L2-resident pass (gfx950).
+//
+// Why.  The SpMM is bound by random 128-B line requests: every nonzero
+// gathers one row of Z.  An fp32 row of F = 32q + r features (1 <= r <= 4: F = 100 is
+// 96 + 4) spans q + 1 lines, and the last one carries only r * 4 <= 16 useful bytes -- a
+// quarter of products-synth's line requests.  Those r columns are taken out of the gather:
+//
+//   * Z between iterations is kept "split": Z_main [n, 32q] (rows of whole lines, so a
+//     gather is exactly q lines) and Z_rem [n, 4] (16 B per row).
+//   * The remainder product  R = (M_k o A_hat) Z_rem  runs as a pass over A_hat blocked by
+//     SOURCE rows: block b holds the entries whose column lies in [b*2^17, (b+1)*2^17), i.e.
+//     2 MB of Z_rem, which stays resident in every XCD's 4 MB L2 while the block's launch
+//     gathers from it.  One launch per block accumulates into R in block order (fixed order:
+//     bitwise deterministic).
+//   * The main kernel gathers the q lines of Z_main per nonzero and takes R as the
+//     remainder lanes' pre-summed accumulator (appnp_spmm.hip wave_row, StepArgs::rem_in).
+//
+// The blocked copy of A_hat (APPNP_GRAPH_SOURCE_BLOCKS) is built at graph creation:
+// sb_ptr[b * rows + i] is the first entry of row i in block b (block-major, row-minor, so the
+// entries of one block are contiguous and one launch streams them once).
+#include <algorithm>
+#include <cstdlib>
+
+#include "appnp_internal.h"
+#include "../../include/ppnp_amd.h"
+
+namespace appnp {
+namespace {
+
+// entries of each (block, row): the row's columns are sorted, so a block is a contiguous run
+__global__ __launch_bounds__(kBlock) void k_sb_count(const int32_t* __restrict__ rp,
+                                                     const int32_t* __restrict__ col, int64_t rows,
+                                                     int shift, int32_t* __restrict__ cnt) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= rows) return;
+  int cur = -1, c = 0;
+  for (int32_t e = rp[i]; e < rp[i + 1]; ++e) {
+    const int b = col[e] >> shift;
+    if (b != cur) {
+      if (cur >= 0) cnt[(int64_t)cur * rows + i] = c;
+      cur = b;
+      c = 0;
+    }
+    ++c;
+  }
+  if (cur >= 0) cnt[(int64_t)cur * rows + i] = c;
+}
+
+__global__ __launch_bounds__(kBlock) void k_sb_fill(const int32_t* __restrict__ rp,
+                                                    const int32_t* __restrict__ col,
+                                                    const float* __restrict__ val, int64_t rows,
+                                                    int shift, const int32_t* __restrict__ ptr,
+                                                    int32_t* __restrict__ bcol,
+                                                    float* __restrict__ bval) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= rows) return;
+  int cur = -1;
+  int32_t pos = 0;
+  for (int32_t e = rp[i]; e < rp[i + 1]; ++e) {
+    const int32_t c = col[e];
+    const int b = c >> shift;
+    if (b != cur) {
+      cur = b;
+      pos = ptr[(int64_t)b * rows + i];
+    }
+    bcol[pos] = c;
+    bval[pos] = val[e];
+    ++pos;
+  }
+}
+
+// R[i] (+)= sum over the entries of row i in source block b of w_ij * Z_rem[j]; thread per
+// row (a block holds ~nnz/(rows * n_sb) entries of a row: 2.7 on products-synth), U entries
+// loaded and gathered at a time so that a wave's longest row takes few dependent rounds.
+// One launch per block, so all resident waves gather from the same 2 MB of Z_rem; per row the
+// sum runs over blocks in order and entries in column order (fixed: bitwise deterministic).
+// a.zin = Z_rem (n x 4 fp32), a.aux = R (rows x 4 fp32 accumulator).  FIRST: R starts at 0.
+// LAST: the iteration's epilogue, out[i, :nv] = (1-alpha) R[i] + alpha H_rem[i] (a.h = H_rem,
+// a.out / a.ld_out, a.f = nv valid columns: 4 into the next Z_rem, 1-4 into Z's last columns).
+// (A single launch keeping every row's sum in registers while all threads walk the blocks
+// measured slower: threads drift apart and the blocks they gather from no longer fit L2.)
+template <int U, bool FIRST, bool LAST>
+__global__ __launch_bounds__(kBlock) void k_rem_block(StepArgs a, const int32_t* __restrict__ ptr,
+                                                      const int32_t* __restrict__ bcol,
+                                                      const float* __restrict__ bval) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= a.n_rows) return;
+  const f32x4* __restrict__ z = static_cast<const f32x4*>(a.zin);
+  f32x4* __restrict__ r = static_cast<f32x4*>(a.aux);
+  f32x4 acc = FIRST ? f32x4{0.0f, 0.0f, 0.0f, 0.0f} : r[i];
+  const int32_t end = ptr[i + 1];
+  for (int32_t e = ptr[i]; e < end; e += U) {
+    int32_t c[U];
+    float w[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      c[u] = 0;
+      w[u] = 0.0f;
+      if (e + u < end) {
+        c[u] = ld_nt<int32_t>(bcol + e + u);
+        w[u] = ld_nt<float>(bval + e + u);
+      }
+    }
+    f32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      v[u] = e + u < end ? z[c[u]] : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const float wu = e + u < end ? edge_weight(w[u], a.row_lo + i, c[u], a) : 0.0f;
+      acc.x = fmaf(wu, v[u].x, acc.x);
+      acc.y = fmaf(wu, v[u].y, acc.y);
+      acc.z = fmaf(wu, v[u].z, acc.z);
+      acc.w = fmaf(wu, v[u].w, acc.w);
+    }
+  }
+  if constexpr (!LAST) {
+    r[i] = acc;
+  } else {
+    // H rows are 16-B aligned with ld_h >= roundup(f, 4): the 16 B at H_rem stay in the row
+    f32x4 h = *reinterpret_cast<const f32x4*>(static_cast<const float*>(a.h) + i * a.ld_h);
+    const int nv = a.f;
+    const float y[4] = {fmaf(a.alpha, h.x, a.scale * acc.x),
+                        fmaf(a.alpha, nv > 1 ? h.y : 0.0f, a.scale * acc.y),
+                        fmaf(a.alpha, nv > 2 ? h.z : 0.0f, a.scale * acc.z),
+                        fmaf(a.alpha, nv > 3 ? h.w : 0.0f, a.scale * acc.w)};
+    float* o = static_cast<float*>(a.out) + i * a.ld_out;
+    if (nv == 4) {
+      *reinterpret_cast<f32x4*>(o) = f32x4{y[0], y[1], y[2], y[3]};
+    } else {
+      for (int v = 0; v < nv; ++v) o[v] = y[v];
+    }
+  }
+}
+
+// H [n, ld_h] -> the split layout: main [n, fs] (whole lines per row) and rem [n, 4]
+// (columns fs..f-1, zero padded).  Thread per 16-B piece of a row (fs / 4 + 1 pieces).
+__global__ __launch_bounds__(kBlock) void k_split_copy(const float* __restrict__ h, int64_t ld_h,
+                                                       int64_t n, int f, int fs,
+                                                       float* __restrict__ main,
+                                                       float* __restrict__ rem) {
+  const int pieces = fs / 4 + 1;
+  const int64_t total = n * pieces;
+  for (int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * kBlock) {
+    const int64_t row = t / pieces;
+    const int q = (int)(t - row * pieces);
+    f32x4 v = ld_nt<f32x4>(h + row * ld_h + 4 * q);
+    if (q < fs / 4) {
+      *reinterpret_cast<f32x4*>(main + row * fs + 4 * q) = v;
+    } else {
+      const int nv = f - fs;
+      if (nv < 4) v.w = 0.0f;
+      if (nv < 3) v.z = 0.0f;
+      if (nv < 2) v.y = 0.0f;
+      *reinterpret_cast<f32x4*>(rem + row * 4) = v;
+    }
+  }
+}
+
+}  // namespace
+
+int graph_build_source_blocks(appnp_graph* g, hipStream_t s) {
+  const int64_t rows = g->row_hi - g->row_lo;
+  static const int shift = [] {
+    const char* v = getenv("APPNP_SB_SHIFT");  // measurement override of kSourceBlockShift
+    const int x = (v && *v) ? atoi(v) : kSourceBlockShift;
+    return x >= 10 && x <= 30 ? x : kSourceBlockShift;
+  }();
+  const int64_t nb = std::max<int64_t>(1, (g->n + (1LL << shift) - 1) >> shift);
+  const int64_t cells = nb * rows;
+  if (cells + 1 > INT32_MAX) return APPNP_ERANGE;
+  int rc = APPNP_OK;
+  int32_t* cnt = nullptr;
+  int64_t *bsum = nullptr, *tot = nullptr;
+  const unsigned grid = (unsigned)std::max<int64_t>(1, (rows + kBlock - 1) / kBlock);
+  auto ok = [&](hipError_t e) {
+    if (e != hipSuccess && rc == APPNP_OK)
+      rc = (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) ? APPNP_ENOMEM
+                                                                       : APPNP_EDEVICE;
+    return rc == APPNP_OK;
+  };
+  if (ok(hipMalloc(&g->sb_ptr, (cells + 1) * sizeof(int32_t))) &&
+      ok(hipMalloc(&g->sb_col, std::max<int64_t>(1, g->nnz_hat) * sizeof(int32_t))) &&
+      ok(hipMalloc(&g->sb_val, std::max<int64_t>(1, g->nnz_hat) * sizeof(float))) &&
+      ok(hipMalloc(&cnt, std::max<int64_t>(1, cells) * sizeof(int32_t))) &&
+      ok(hipMalloc(&bsum, scan_partials(cells) * sizeof(int64_t))) &&
+      ok(hipMalloc(&tot, sizeof(int64_t))) &&
+      ok(hipMemsetAsync(cnt, 0, std::max<int64_t>(1, cells) * sizeof(int32_t), s))) {
+    if (rows > 0) {
+      hipLaunchKernelGGL(k_sb_count, dim3(grid), dim3(kBlock), 0, s, g->row_ptr, g->col, rows,
+                         shift, cnt);
+      ok(hipGetLastError());
+    }
+    if (rc == APPNP_OK && ok(exclusive_scan(cnt, cells, g->sb_ptr, bsum, tot, s)) && rows > 0) {
+      hipLaunchKernelGGL(k_sb_fill, dim3(grid), dim3(kBlock), 0, s, g->row_ptr, g->col, g->val,
+                         rows, shift, g->sb_ptr, g->sb_col, g->sb_val);
+      ok(hipGetLastError());
+    }
+    if (rc == APPNP_OK) ok(hipStreamSynchronize(s));
+  }
+  if (cnt) (void)hipFree(cnt);
+  if (bsum) (void)hipFree(bsum);
+  if (tot) (void)hipFree(tot);
+  if (rc != APPNP_OK) {
+    if (g->sb_ptr) (void)hipFree(g->sb_ptr);
+    if (g->sb_col) (void)hipFree(g->sb_col);
+    if (g->sb_val) (void)hipFree(g->sb_val);
+    g->sb_ptr = g->sb_col = nullptr;
+    g->sb_val = nullptr;
+    return rc;
+  }
+  g->n_sb = (int32_t)nb;
+  return APPNP_OK;
+}
+
+// One iteration of the remainder columns: R = (M_k o A_hat) Z_rem over all source blocks, one
+// launch per block in block order, the last one applying the epilogue (k_rem_block).
+// a: the iteration's StepArgs (dropout key, row_lo, n_rows, scale, alpha); z_rem [n, 4];
+// acc [rows, 4] scratch (may be `out` itself when out is a Z_rem buffer); h_rem = H + fs;
+// out / ld_out / nv: where the nv valid columns of Z_{k+1} go.
+// Entries in flight per thread: 8 (1 measured 1.6 ms per products-synth iteration, 8 1.4 ms).
+hipError_t launch_remainder(const appnp_graph* g, const StepArgs& a_in, const float* z_rem,
+                            float* acc, const float* h_rem, int64_t ld_h, float* out,
+                            int64_t ld_out, int nv, hipStream_t s) {
+  StepArgs a = a_in;
+  a.zin = z_rem;
+  a.aux = acc;
+  a.h = h_rem;
+  a.ld_h = ld_h;
+  a.out = out;
+  a.ld_out = ld_out;
+  a.f = nv;
+  const int64_t rows = a.n_rows;
+  if (rows <= 0) return hipSuccess;
+  const dim3 grid((unsigned)((rows + kBlock - 1) / kBlock)), block(kBlock);
+  const int nb = g->n_sb;
+  for (int32_t b = 0; b < nb; ++b) {
+    const int32_t* p = g->sb_ptr + (int64_t)b * rows;
+    if (nb == 1)
+      hipLaunchKernelGGL((k_rem_block<8, true, true>), grid, block, 0, s, a, p, g->sb_col,
+                         g->sb_val);
+    else if (b == 0)
+      hipLaunchKernelGGL((k_rem_block<8, true, false>), grid, block, 0, s, a, p, g->sb_col,
+                         g->sb_val);
+    else if (b == nb - 1)
+      hipLaunchKernelGGL((k_rem_block<8, false, true>), grid, block, 0, s, a, p, g->sb_col,
+                         g->sb_val);
+    else
+      hipLaunchKernelGGL((k_rem_block<8, false, false>), grid, block, 0, s, a, p, g->sb_col,
+                         g->sb_val);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_split_copy(const float* h, int64_t ld_h, int64_t n, int64_t f, int64_t fs,
+                             float* main, float* rem, hipStream_t s) {
+  const int64_t total = n * (fs / 4 + 1);
+  if (total <= 0) return hipSuccess;
+  const int64_t blocks = std::min<int64_t>((total + kBlock - 1) / kBlock, 1 << 20);
+  hipLaunchKernelGGL(k_split_copy, dim3((unsigned)blocks), dim3(kBlock), 0, s, h, ld_h, n,
+                     (int)f, (int)fs, main, rem);
+  return hipGetLastError();
+}
+
+}  // namespace appnp

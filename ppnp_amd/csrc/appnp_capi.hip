@@ -3,6 +3,7 @@
 // Argument validation, workspace ping-pong and the K-iteration launch sequence.  No host
 // synchronisation or allocation happens in appnp_propagate / appnp_propagate_bwd /
 // appnp_step, so a caller may capture them in a hipGraph.
+#include <cstdlib>
 #include <new>
 
 #include "../../include/ppnp_amd.h"
@@ -105,6 +106,68 @@ StepArgs base_args(const appnp_graph* g, int64_t f, float alpha) {
   return a;
 }
 
+int env_flag(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return (v && *v) ? atoi(v) : dflt;
+}
+
+// Split rows (appnp_blocks.hip): fp32 rows of F = 32q + r features, 1 <= r <= 4, gather q whole
+// lines from the split layout [n, 32q]; the r remainder columns run as a separate chain of
+// L2-resident passes over the source-blocked A_hat.  Returns the split point 32q, or 0 when the path does
+// not apply (no blocked copy, bf16, latency-regime graph, F outside (32, 256], vectors
+// narrower than 16 B).  APPNP_SPLIT=0 disables it (measurement).
+int64_t split_point(const appnp_graph* g, int64_t f, int dtype, int V) {
+  static const int enabled = env_flag("APPNP_SPLIT", 1);
+  if (!enabled || !g->sb_ptr || dtype != APPNP_F32 || V != 4) return 0;
+  if (g->n <= (1 << 16) || f <= 32 || f > 256) return 0;
+  const int64_t r = f % 32;
+  return (r >= 1 && r <= 4) ? f - r : 0;
+}
+
+// The forward loop in the split layout (appnp_blocks.hip).  Propagation is column-separable,
+// so the main columns [0, fs) and the remainder columns [fs, f) are two independent K-step
+// chains that meet only in Z:
+//   * H is copied once into split buffer 0 (main part [n, fs], remainder part [n, 4]);
+//   * main chain: K launches of the SpMM kernel on fs columns, gathering whole lines of the
+//     main parts (ping-pong between the two buffers, the last into Z[:, :fs]);
+//   * remainder chain: K L2-blocked passes over the remainder parts (the last into Z[:, fs:f]).
+// The chains touch disjoint parts of the buffers and disjoint columns of Z.  Both run on the
+// caller's stream: on a side stream they overlapped in time but shared the memory system, and
+// the total measured within 1 % of running them one after the other.
+int propagate_split(const appnp_graph* g, const StepArgs& a0, const void* H, int64_t ld_h,
+                    void* Z, int64_t ld_z, int64_t fs, int K, float p_drop, uint64_t seed,
+                    char* ws, int64_t main_b, int64_t buf_b, hipStream_t s) {
+  const int64_t n = a0.n_rows, f = a0.f;
+  char* bufs[2] = {ws, ws + buf_b};
+  auto main_of = [&](int i) { return reinterpret_cast<float*>(bufs[i]); };
+  auto rem_of = [&](int i) { return reinterpret_cast<float*>(bufs[i] + main_b); };
+  const float* h = static_cast<const float*>(H);
+  float* z = static_cast<float*>(Z);
+  int rc = dev_err(appnp::launch_split_copy(h, ld_h, n, f, fs, main_of(0), rem_of(0), s));
+  StepArgs am = a0, ar = a0;  // main / remainder chain
+  am.f = (int32_t)fs;
+  am.h = H;
+  am.ld_h = ld_h;
+  am.ld_in = fs;
+  int cur = 0;
+  for (int k = 0; k < K && !rc; ++k) {
+    const int dst = cur ^ 1;
+    const bool last = k == K - 1;
+    set_drop(am, p_drop, seed, k);
+    am.zin = main_of(cur);
+    am.out = last ? Z : main_of(dst);
+    am.ld_out = last ? ld_z : fs;
+    rc = dev_err(appnp::launch_step(APPNP_F32, appnp::EPI_FWD, 4, am, s));
+    if (rc) break;
+    set_drop(ar, p_drop, seed, k);
+    rc = dev_err(appnp::launch_remainder(g, ar, rem_of(cur), rem_of(dst), h + fs, ld_h,
+                                         last ? z + fs : rem_of(dst), last ? ld_z : 4,
+                                         last ? (int)(f - fs) : 4, s));
+    cur = dst;
+  }
+  return rc;
+}
+
 }  // namespace
 
 extern "C" {
@@ -130,7 +193,8 @@ int appnp_graph_create_rows(const int32_t* indptr, const int32_t* indices, const
   *out = nullptr;
   if (n < 0 || nnz < 0 || n > INT32_MAX || nnz > INT32_MAX) return n > INT32_MAX || nnz > INT32_MAX ? APPNP_ERANGE : APPNP_EINVAL;
   const bool want_t = (mode & APPNP_GRAPH_TRANSPOSE) != 0;
-  mode &= ~APPNP_GRAPH_TRANSPOSE;
+  const bool want_sb = (mode & APPNP_GRAPH_SOURCE_BLOCKS) != 0;
+  mode &= ~(APPNP_GRAPH_TRANSPOSE | APPNP_GRAPH_SOURCE_BLOCKS);
   if (mode != APPNP_NORM_SYM && mode != APPNP_NORM_RW) return APPNP_EINVAL;
   if (row_lo < 0 || row_hi < row_lo || row_hi > n) return APPNP_EINVAL;
   if (want_t && (row_lo != 0 || row_hi != n)) return APPNP_EINVAL;
@@ -143,6 +207,9 @@ int appnp_graph_create_rows(const int32_t* indptr, const int32_t* indices, const
   // A_hat^T for the adjoint, unless A_hat is symmetric already ('sym' on undirected A)
   if (rc == APPNP_OK && want_t && !(g->mode == APPNP_NORM_SYM && g->symmetric))
     rc = appnp::graph_build_transpose(g, as_stream(stream));
+  // source-blocked copy for the remainder pass (full graphs; appnp_propagate uses it)
+  if (rc == APPNP_OK && want_sb && row_lo == 0 && row_hi == n)
+    rc = appnp::graph_build_source_blocks(g, as_stream(stream));
   if (rc != APPNP_OK) {
     appnp::graph_free(g);
     delete g;
@@ -211,8 +278,15 @@ size_t appnp_workspace_bytes(const appnp_graph* g, int64_t f, int64_t ld, int dt
   if (!g || f < 0 || !valid_dtype(dtype)) return 0;
   (void)ld;  // the workspace uses its own line-aligned leading dimension
   const int64_t rows = g->row_hi - g->row_lo;
-  // two ping-pong buffers (the forward needs one, the adjoint two), 256-B aligned
-  return (size_t)(2 * rows * line_ld(f, dtype) * elem_size(dtype) + 256);
+  // two ping-pong buffers (the forward needs one -- two in the split layout, each as large
+  // as a packed buffer -- the adjoint two), 256-B aligned each
+  return (size_t)(2 * rows * line_ld(f, dtype) * elem_size(dtype) + 2048);
+}
+
+int appnp_propagate_split_point(const appnp_graph* g, int64_t f, int dtype, int64_t* fs) {
+  if (!g || !fs || f < 0 || !valid_dtype(dtype)) return APPNP_EINVAL;
+  *fs = split_point(g, f, dtype, dtype == APPNP_F32 ? 4 : 8);
+  return APPNP_OK;
 }
 
 int appnp_propagate(const appnp_graph* g, const void* H, int64_t ld_h, void* Z, int64_t ld_z,
@@ -230,6 +304,7 @@ int appnp_propagate(const appnp_graph* g, const void* H, int64_t ld_h, void* Z, 
     return dev_err(hipMemcpy2DAsync(Z, ld_z * es, H, ld_h * es, f * es, n,
                                     hipMemcpyDeviceToDevice, s));
   const int64_t ld_w = line_ld(f, dtype);
+  void* const ws_orig = ws;
   if (K >= 2) {
     if (!ws) return APPNP_EINVAL;
     const uintptr_t base = reinterpret_cast<uintptr_t>(ws);
@@ -244,6 +319,17 @@ int appnp_propagate(const appnp_graph* g, const void* H, int64_t ld_h, void* Z, 
   StepArgs a = base_args(g, f, alpha);
   a.h = H;
   a.ld_h = ld_h;
+  const int64_t fs = K >= 2 ? split_point(g, f, dtype, V) : 0;
+  if (fs > 0) {
+    // two split buffers [n, fs] + [n, 4] fp32 in the workspace, each 256-B aligned
+    const int64_t main_b = (n * fs * 4 + 255) / 256 * 256;
+    const int64_t buf_b = (main_b + n * 16 + 255) / 256 * 256;
+    const size_t used = (size_t)(reinterpret_cast<uintptr_t>(ws) -
+                                 reinterpret_cast<uintptr_t>(ws_orig));
+    if (ws_bytes >= used + 2 * (size_t)buf_b)
+      return propagate_split(g, a, H, ld_h, Z, ld_z, fs, K, p_drop, seed,
+                             static_cast<char*>(ws), main_b, buf_b, s);
+  }
   const void* src = H;
   int64_t ld_src = ld_h;
   for (int k = 0; k < K; ++k) {

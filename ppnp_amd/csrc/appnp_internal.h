@@ -37,6 +37,10 @@ struct appnp_graph {
   int32_t* t_row_ptr = nullptr; // A_hat^T (APPNP_GRAPH_TRANSPOSE, when A_hat is not symmetric)
   int32_t* t_col = nullptr;
   float* t_val = nullptr;
+  int32_t* sb_ptr = nullptr;    // A_hat blocked by source rows (APPNP_GRAPH_SOURCE_BLOCKS):
+  int32_t* sb_col = nullptr;    //   [n_sb * rows + 1], block-major (appnp_blocks.hip)
+  float* sb_val = nullptr;
+  int32_t n_sb = 0;
 };
 
 struct appnp_csr;
@@ -59,6 +63,14 @@ int csr_transpose(const int32_t* indptr, const int32_t* indices, const float* va
 void csr_free(appnp_csr* c);
 hipError_t exclusive_scan(const int32_t* cnt, int64_t rows, int32_t* out, int64_t* d_bsum,
                           int64_t* d_total, hipStream_t s);
+
+// appnp_blocks.hip
+int graph_build_source_blocks(appnp_graph* g, hipStream_t s);
+hipError_t launch_remainder(const appnp_graph* g, const StepArgs& a, const float* z_rem,
+                            float* acc, const float* h_rem, int64_t ld_h, float* out,
+                            int64_t ld_out, int nv, hipStream_t s);
+hipError_t launch_split_copy(const float* h, int64_t ld_h, int64_t n, int64_t f, int64_t fs,
+                             float* main, float* rem, hipStream_t s);
 
 // appnp_spmm.hip
 int pick_vec(int dtype, int64_t f, const int64_t* lds, int n_ld, const void* const* ptrs,

@@ -368,6 +368,7 @@ hipError_t launch_g(int G, bool wide, int uw, dim3 grid, const StepArgs& a, hipS
   if (wide) {
     if (uw == 8) return launch_wide<T, V, EPI, TAIL, 8>(G, grid, a, s);
     if (uw == 4) return launch_wide<T, V, EPI, TAIL, 4>(G, grid, a, s);
+    if (uw == 2) return launch_wide<T, V, EPI, TAIL, 2>(G, grid, a, s);
     return launch_wide<T, V, EPI, TAIL, 1>(G, grid, a, s);
   }
   const dim3 block(kBlock);
@@ -475,14 +476,15 @@ hipError_t launch_step(int dtype, int epi, int V, const StepArgs& a_in, hipStrea
     a.n_heavy = 0;
   }
   const dim3 grid((unsigned)blocks, (unsigned)slabs);
-  // entries in flight per sub-group of the wide kernel.  Bandwidth regime: 1 -- occupancy
-  // supplies the memory-level parallelism; measured equal (products fp32) or faster (arxiv
-  // fp32 +3 %, bf16 +9-19 %) than 2, 4 or 8, which cost VGPRs.  Small graphs with long rows
-  // (latency regime, wave per row because of them): 8, so the longest row -- which sets the
-  // launch time -- takes few dependent rounds (Cora-ML 9.4 -> 5.8 us, Citeseer 5.4 -> 3.9 us
-  // per iteration; tools/sweep_uw_latency.sh).
-  static const int uw_env = env_int("APPNP_UW", -1);  // measurement override (1, 4, 8)
-  const int uw = uw_env > 0 ? uw_env : (latency && heavy_rows) ? 8 : 1;
+  // entries in flight per sub-group of the wide kernel (tools/sweep_uw_bw.sh,
+  // tools/sweep_uw.sh).  Bandwidth regime with long rows (>= kWideAvgRow on average): 2 --
+  // products-synth fp32 F = 96 8.20 -> 7.32 ms, F = 100 9.76 -> 9.57, products-powerlaw
+  // 9.84 -> 9.06, bf16 and F = 128 +0.4-1 %; 4 is no better and costs VGPRs.  Short rows
+  // (arxiv-synth, 14.8 a row): 1, 3 % faster than 2.  Small graphs with hub rows (latency
+  // regime, wave per row because of them): 8, so the longest row -- which sets the launch
+  // time -- takes few dependent rounds (Cora-ML 9.4 -> 5.8 us, Citeseer 5.4 -> 3.9 us).
+  static const int uw_env = env_int("APPNP_UW", -1);  // measurement override (1, 2, 4, 8)
+  const int uw = uw_env > 0 ? uw_env : (latency && heavy_rows) ? 8 : (!latency && long_rows) ? 2 : 1;
   // cache policy of the streams (StepArgs::nt); APPNP_NT overrides for measurement
   static const int nt_env = env_int("APPNP_NT", -1);
   a.nt = nt_env >= 0 ? nt_env : (latency ? 0 : 1);

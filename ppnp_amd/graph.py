@@ -48,10 +48,13 @@ class Graph:
     # -- construction ---------------------------------------------------------------------
     @classmethod
     def from_csr(cls, indptr, indices, data, n, mode="sym", device=None, row_lo=0,
-                 row_hi=None, split_local=False, transpose=False):
+                 row_hi=None, split_local=False, transpose=False, source_blocks=None):
         """indptr/indices (int32) and optional data (fp32) of A; tensors or arrays.
         ``transpose=True`` also builds A_hat^T when A_hat is not symmetric (rw mode or a
-        directed graph), which the backward needs."""
+        directed graph), which the backward needs.  ``source_blocks`` keeps the copy of A_hat
+        blocked by source rows that lets fp32 rows of F = 32q + r (r <= 4) features gather q
+        cache lines instead of q + 1 (APPNP_GRAPH_SOURCE_BLOCKS); default: full graphs above
+        the latency regime (n > 65536)."""
         if mode not in _lib.NORM:
             raise ValueError(f"mode must be 'sym' or 'rw', got {mode!r}")
         device = torch.device(device if device is not None else "cuda")
@@ -72,12 +75,16 @@ class Graph:
             raise ValueError("indptr must have n+1 entries")
         nnz = int(ix.numel())
         row_hi = n if row_hi is None else int(row_hi)
+        if source_blocks is None:
+            source_blocks = n > (1 << 16) and int(row_lo) == 0 and row_hi == n
+        flags = ((_lib.GRAPH_TRANSPOSE if transpose else 0)
+                 | (_lib.GRAPH_SOURCE_BLOCKS if source_blocks else 0))
         lib = _lib.load()
         out = C.c_void_p()
         with torch.cuda.device(device):
             rc = lib.appnp_graph_create_rows(
                 _ptr(ip), _ptr(ix), _ptr(dv), n, nnz,
-                _lib.NORM[mode] | (_lib.GRAPH_TRANSPOSE if transpose else 0), int(row_lo), row_hi,
+                _lib.NORM[mode] | flags, int(row_lo), row_hi,
                 1 if split_local else 0, C.c_void_p(_stream_ptr(device)), C.byref(out),
             )
         _lib.check("appnp_graph_create", rc)
@@ -102,6 +109,15 @@ class Graph:
     @property
     def rows(self) -> int:
         return self.row_hi - self.row_lo
+
+    def split_point(self, f: int, dtype=torch.float32) -> int:
+        """Columns [0, fs) that appnp_propagate gathers as whole cache lines when the rest run
+        the L2-blocked remainder pass (appnp_propagate_split_point); 0: rows gathered whole."""
+        fs = C.c_int64()
+        dt = _lib.BF16 if dtype == torch.bfloat16 else _lib.F32
+        _lib.check("appnp_propagate_split_point",
+                   _lib.load().appnp_propagate_split_point(self._h, int(f), dt, C.byref(fs)))
+        return fs.value
 
     def csr(self):
         """(row_ptr int32, col int32, val fp32, dinv fp64) as new device tensors."""
