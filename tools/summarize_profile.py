@@ -30,6 +30,7 @@ def find(d, suffix):
 
 
 def per_dispatch(path, match):
+    """{counter: [value per dispatch]} for the kernels whose name contains ``match``."""
     vals = collections.defaultdict(float)
     names = {}
     for r in csv.DictReader(open(path)):
@@ -42,13 +43,27 @@ def per_dispatch(path, match):
     return out, names
 
 
+def per_iteration(path, counter, kernels):
+    """Counter total of one APPNP iteration: the sum over the dispatches of every kernel of
+    the iteration (the SpMM kernel first; with split rows also the remainder passes and the
+    per-call split copy) divided by the number of SpMM dispatches (one per iteration)."""
+    total, n_iter = 0.0, 0
+    for i, k in enumerate(kernels):
+        d, _ = per_dispatch(path, k)
+        total += sum(d[counter])
+        if i == 0:
+            n_iter = len(d[counter])
+    return total / max(1, n_iter), n_iter
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("tag")
     p.add_argument("stats_dir")
     p.add_argument("fetch_dir")
     p.add_argument("write_dir")
-    p.add_argument("--kernel", default="k_step_")
+    p.add_argument("--kernels", default="k_step_,k_rem_block,k_split_copy",
+                   help="kernels of one iteration, the SpMM kernel (one per iteration) first")
     p.add_argument("--workload", default="products-synth")
     p.add_argument("--bench-json", default=None)
     a = p.parse_args()
@@ -57,11 +72,13 @@ def main():
     stats = find(a.stats_dir, "kernel_stats.csv")
     shutil.copy(stats, os.path.join(prof, f"{a.tag}_kernel_stats.csv"))
     rows = list(csv.DictReader(open(stats)))
-    kern = [r for r in rows if a.kernel in r["Name"]]
-    fetch, _ = per_dispatch(find(a.fetch_dir, "counter_collection.csv"), a.kernel)
-    write, _ = per_dispatch(find(a.write_dir, "counter_collection.csv"), a.kernel)
-    f_kib = sum(fetch["FETCH_SIZE"]) / max(1, len(fetch["FETCH_SIZE"]))
-    w_kib = sum(write["WRITE_SIZE"]) / max(1, len(write["WRITE_SIZE"]))
+    kernels = a.kernels.split(",")
+    kern = [r for r in rows if any(k in r["Name"] for k in kernels)]
+    spmm_calls = sum(int(r["Calls"]) for r in kern if kernels[0] in r["Name"])
+    iter_ns = sum(float(r["TotalDurationNs"]) for r in kern) / max(1, spmm_calls)
+    f_kib, n_iter = per_iteration(find(a.fetch_dir, "counter_collection.csv"), "FETCH_SIZE",
+                                  kernels)
+    w_kib, _ = per_iteration(find(a.write_dir, "counter_collection.csv"), "WRITE_SIZE", kernels)
     fetch_b = 2.0 * f_kib * 1024
     write_b = w_kib * 1024
     summ = {
@@ -71,10 +88,13 @@ def main():
             {"name": r["Name"], "calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
              "pct": float(r["Percentage"])} for r in kern
         ],
+        # kernel time of one iteration (all its kernels), comparable to bench avg_launch_ms
+        "iteration_ms": iter_ns / 1e6,
         "pmc": {
             "FETCH_SIZE_KiB_per_launch": f_kib,
             "WRITE_SIZE_KiB_per_launch": w_kib,
-            "launches": len(fetch["FETCH_SIZE"]),
+            "per": "iteration (SpMM launch + remainder passes + split copy / K)",
+            "launches": n_iter,
             "fetch_bytes_corrected": fetch_b,
             "write_bytes": write_b,
             "traffic_bytes_per_launch": fetch_b + write_b,
