@@ -79,14 +79,75 @@ __global__ __launch_bounds__(kBlock) void k_sb_fill(const int32_t* __restrict__ 
 // a.out / a.ld_out, a.f = nv valid columns: 4 into the next Z_rem, 1-4 into Z's last columns).
 // (A single launch keeping every row's sum in registers while all threads walk the blocks
 // measured slower: threads drift apart and the blocks they gather from no longer fit L2.)
+template <bool FIRST, bool LAST>
+__device__ __forceinline__ void rem_finish(const StepArgs& a, int64_t i, f32x4 acc) {
+  if constexpr (!LAST) {
+    static_cast<f32x4*>(a.aux)[i] = acc;
+  } else {
+    // H rows are 16-B aligned with ld_h >= roundup(f, 4): the 16 B at H_rem stay in the row
+    f32x4 h = *reinterpret_cast<const f32x4*>(static_cast<const float*>(a.h) + i * a.ld_h);
+    const int nv = a.f;
+    const float y[4] = {fmaf(a.alpha, h.x, a.scale * acc.x),
+                        fmaf(a.alpha, nv > 1 ? h.y : 0.0f, a.scale * acc.y),
+                        fmaf(a.alpha, nv > 2 ? h.z : 0.0f, a.scale * acc.z),
+                        fmaf(a.alpha, nv > 3 ? h.w : 0.0f, a.scale * acc.w)};
+    float* o = static_cast<float*>(a.out) + i * a.ld_out;
+    if (nv == 4) {
+      *reinterpret_cast<f32x4*>(o) = f32x4{y[0], y[1], y[2], y[3]};
+    } else {
+      for (int v = 0; v < nv; ++v) o[v] = y[v];
+    }
+  }
+}
+
+// Blocks [0, light_blocks): thread per row.  Trailing blocks: hub rows (> kHubRow entries in
+// all, listed in a.hub; the light threads skip them), a wavefront each -- its lanes stride
+// over the row's entries of the block and a fixed butterfly adds them -- so a power-law hub
+// does not serialise one thread while the launch waits.
 template <int U, bool FIRST, bool LAST>
 __global__ __launch_bounds__(kBlock) void k_rem_block(StepArgs a, const int32_t* __restrict__ ptr,
                                                       const int32_t* __restrict__ bcol,
                                                       const float* __restrict__ bval) {
+  const f32x4* __restrict__ z = static_cast<const f32x4*>(a.zin);
+  const f32x4* __restrict__ r = static_cast<const f32x4*>(a.aux);
+  if ((int64_t)blockIdx.x >= a.light_blocks) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t nw = ((int64_t)gridDim.x - a.light_blocks) * kWavesPerBlock;
+    for (int64_t hw = ((int64_t)blockIdx.x - a.light_blocks) * kWavesPerBlock +
+                      (threadIdx.x >> 6);
+         hw < a.n_hub; hw += nw) {
+      const int64_t i = a.hub[hw];
+      f32x4 acc = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+      const int32_t end = ptr[i + 1];
+      for (int32_t e = ptr[i] + lane; e < end; e += kWave) {
+        const int32_t c = ld_nt<int32_t>(bcol + e);
+        const float w = edge_weight(ld_nt<float>(bval + e), a.row_lo + i, c, a);
+        const f32x4 v = z[c];
+        acc.x = fmaf(w, v.x, acc.x);
+        acc.y = fmaf(w, v.y, acc.y);
+        acc.z = fmaf(w, v.z, acc.z);
+        acc.w = fmaf(w, v.w, acc.w);
+      }
+#pragma unroll
+      for (int off = 1; off < kWave; off <<= 1) {
+        acc.x += __shfl_xor(acc.x, off);
+        acc.y += __shfl_xor(acc.y, off);
+        acc.z += __shfl_xor(acc.z, off);
+        acc.w += __shfl_xor(acc.w, off);
+      }
+      if (lane == 0) {
+        if constexpr (!FIRST) {
+          const f32x4 p = r[i];
+          acc = f32x4{p.x + acc.x, p.y + acc.y, p.z + acc.z, p.w + acc.w};
+        }
+        rem_finish<FIRST, LAST>(a, i, acc);
+      }
+    }
+    return;
+  }
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= a.n_rows) return;
-  const f32x4* __restrict__ z = static_cast<const f32x4*>(a.zin);
-  f32x4* __restrict__ r = static_cast<f32x4*>(a.aux);
+  if (a.n_hub && a.row_ptr[i + 1] - a.row_ptr[i] > kHubRow) return;  // a trailing block's
   f32x4 acc = FIRST ? f32x4{0.0f, 0.0f, 0.0f, 0.0f} : r[i];
   const int32_t end = ptr[i + 1];
   for (int32_t e = ptr[i]; e < end; e += U) {
@@ -114,23 +175,7 @@ __global__ __launch_bounds__(kBlock) void k_rem_block(StepArgs a, const int32_t*
       acc.w = fmaf(wu, v[u].w, acc.w);
     }
   }
-  if constexpr (!LAST) {
-    r[i] = acc;
-  } else {
-    // H rows are 16-B aligned with ld_h >= roundup(f, 4): the 16 B at H_rem stay in the row
-    f32x4 h = *reinterpret_cast<const f32x4*>(static_cast<const float*>(a.h) + i * a.ld_h);
-    const int nv = a.f;
-    const float y[4] = {fmaf(a.alpha, h.x, a.scale * acc.x),
-                        fmaf(a.alpha, nv > 1 ? h.y : 0.0f, a.scale * acc.y),
-                        fmaf(a.alpha, nv > 2 ? h.z : 0.0f, a.scale * acc.z),
-                        fmaf(a.alpha, nv > 3 ? h.w : 0.0f, a.scale * acc.w)};
-    float* o = static_cast<float*>(a.out) + i * a.ld_out;
-    if (nv == 4) {
-      *reinterpret_cast<f32x4*>(o) = f32x4{y[0], y[1], y[2], y[3]};
-    } else {
-      for (int v = 0; v < nv; ++v) o[v] = y[v];
-    }
-  }
+  rem_finish<FIRST, LAST>(a, i, acc);
 }
 
 // H [n, ld_h] -> the split layout: main [n, fs] (whole lines per row) and rem [n, 4]
@@ -233,7 +278,12 @@ hipError_t launch_remainder(const appnp_graph* g, const StepArgs& a_in, const fl
   a.f = nv;
   const int64_t rows = a.n_rows;
   if (rows <= 0) return hipSuccess;
-  const dim3 grid((unsigned)((rows + kBlock - 1) / kBlock)), block(kBlock);
+  a.row_ptr = g->row_ptr;  // whole-row lengths: hub rows are left to the trailing blocks
+  a.hub = g->hub;
+  a.n_hub = g->hub ? g->n_hub : 0;
+  a.light_blocks = (rows + kBlock - 1) / kBlock;
+  const int64_t heavy = std::min<int64_t>((a.n_hub + kWavesPerBlock - 1) / kWavesPerBlock, 4096);
+  const dim3 grid((unsigned)(a.light_blocks + heavy)), block(kBlock);
   const int nb = g->n_sb;
   for (int32_t b = 0; b < nb; ++b) {
     const int32_t* p = g->sb_ptr + (int64_t)b * rows;
