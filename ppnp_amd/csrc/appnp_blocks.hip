@@ -30,12 +30,12 @@ namespace {
 // entries of each (block, row): the row's columns are sorted, so a block is a contiguous run
 __global__ __launch_bounds__(kBlock) void k_sb_count(const int32_t* __restrict__ rp,
                                                      const int32_t* __restrict__ col, int64_t rows,
-                                                     int shift, int32_t* __restrict__ cnt) {
+                                                     int brows, int32_t* __restrict__ cnt) {
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= rows) return;
   int cur = -1, c = 0;
   for (int32_t e = rp[i]; e < rp[i + 1]; ++e) {
-    const int b = col[e] >> shift;
+    const int b = col[e] / brows;
     if (b != cur) {
       if (cur >= 0) cnt[(int64_t)cur * rows + i] = c;
       cur = b;
@@ -49,7 +49,7 @@ __global__ __launch_bounds__(kBlock) void k_sb_count(const int32_t* __restrict__
 __global__ __launch_bounds__(kBlock) void k_sb_fill(const int32_t* __restrict__ rp,
                                                     const int32_t* __restrict__ col,
                                                     const float* __restrict__ val, int64_t rows,
-                                                    int shift, const int32_t* __restrict__ ptr,
+                                                    int brows, const int32_t* __restrict__ ptr,
                                                     int32_t* __restrict__ bcol,
                                                     float* __restrict__ bval) {
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -58,7 +58,7 @@ __global__ __launch_bounds__(kBlock) void k_sb_fill(const int32_t* __restrict__ 
   int32_t pos = 0;
   for (int32_t e = rp[i]; e < rp[i + 1]; ++e) {
     const int32_t c = col[e];
-    const int b = c >> shift;
+    const int b = c / brows;
     if (b != cur) {
       cur = b;
       pos = ptr[(int64_t)b * rows + i];
@@ -207,12 +207,12 @@ __global__ __launch_bounds__(kBlock) void k_split_copy(const float* __restrict__
 
 int graph_build_source_blocks(appnp_graph* g, hipStream_t s) {
   const int64_t rows = g->row_hi - g->row_lo;
-  static const int shift = [] {
-    const char* v = getenv("APPNP_SB_SHIFT");  // measurement override of kSourceBlockShift
-    const int x = (v && *v) ? atoi(v) : kSourceBlockShift;
-    return x >= 10 && x <= 30 ? x : kSourceBlockShift;
+  static const int brows = [] {
+    const char* v = getenv("APPNP_SB_ROWS");  // measurement override of kSourceBlockRows
+    const int x = (v && *v) ? atoi(v) : kSourceBlockRows;
+    return x >= 1024 ? x : kSourceBlockRows;
   }();
-  const int64_t nb = std::max<int64_t>(1, (g->n + (1LL << shift) - 1) >> shift);
+  const int64_t nb = std::max<int64_t>(1, (g->n + brows - 1) / brows);
   const int64_t cells = nb * rows;
   if (cells + 1 > INT32_MAX) return APPNP_ERANGE;
   int rc = APPNP_OK;
@@ -234,12 +234,12 @@ int graph_build_source_blocks(appnp_graph* g, hipStream_t s) {
       ok(hipMemsetAsync(cnt, 0, std::max<int64_t>(1, cells) * sizeof(int32_t), s))) {
     if (rows > 0) {
       hipLaunchKernelGGL(k_sb_count, dim3(grid), dim3(kBlock), 0, s, g->row_ptr, g->col, rows,
-                         shift, cnt);
+                         brows, cnt);
       ok(hipGetLastError());
     }
     if (rc == APPNP_OK && ok(exclusive_scan(cnt, cells, g->sb_ptr, bsum, tot, s)) && rows > 0) {
       hipLaunchKernelGGL(k_sb_fill, dim3(grid), dim3(kBlock), 0, s, g->row_ptr, g->col, g->val,
-                         rows, shift, g->sb_ptr, g->sb_col, g->sb_val);
+                         rows, brows, g->sb_ptr, g->sb_col, g->sb_val);
       ok(hipGetLastError());
     }
     if (rc == APPNP_OK) ok(hipStreamSynchronize(s));
@@ -264,7 +264,9 @@ int graph_build_source_blocks(appnp_graph* g, hipStream_t s) {
 // a: the iteration's StepArgs (dropout key, row_lo, n_rows, scale, alpha); z_rem [n, 4];
 // acc [rows, 4] scratch (may be `out` itself when out is a Z_rem buffer); h_rem = H + fs;
 // out / ld_out / nv: where the nv valid columns of Z_{k+1} go.
-// Entries in flight per thread: 8 (1 measured 1.6 ms per products-synth iteration, 8 1.4 ms).
+// Entries in flight per thread: 16 (products-synth per iteration: 1 -> 1.6 ms, 8 -> 1.4 ms,
+// 16 0.05 ms less; tools/sweep_split.sh).  Blocks of 2^17 source rows measured best
+// (2^16, 96k, 160k, 192k and 2^18 rows: +0.01-0.3 ms).
 hipError_t launch_remainder(const appnp_graph* g, const StepArgs& a_in, const float* z_rem,
                             float* acc, const float* h_rem, int64_t ld_h, float* out,
                             int64_t ld_out, int nv, hipStream_t s) {
@@ -287,18 +289,14 @@ hipError_t launch_remainder(const appnp_graph* g, const StepArgs& a_in, const fl
   const int nb = g->n_sb;
   for (int32_t b = 0; b < nb; ++b) {
     const int32_t* p = g->sb_ptr + (int64_t)b * rows;
-    if (nb == 1)
-      hipLaunchKernelGGL((k_rem_block<8, true, true>), grid, block, 0, s, a, p, g->sb_col,
-                         g->sb_val);
-    else if (b == 0)
-      hipLaunchKernelGGL((k_rem_block<8, true, false>), grid, block, 0, s, a, p, g->sb_col,
-                         g->sb_val);
-    else if (b == nb - 1)
-      hipLaunchKernelGGL((k_rem_block<8, false, true>), grid, block, 0, s, a, p, g->sb_col,
-                         g->sb_val);
-    else
-      hipLaunchKernelGGL((k_rem_block<8, false, false>), grid, block, 0, s, a, p, g->sb_col,
-                         g->sb_val);
+    const bool first = b == 0, last = b == nb - 1;
+    auto go = [&](auto kern) {
+      hipLaunchKernelGGL(kern, grid, block, 0, s, a, p, g->sb_col, g->sb_val);
+    };
+    if (first && last) go(k_rem_block<16, true, true>);
+    else if (first) go(k_rem_block<16, true, false>);
+    else if (last) go(k_rem_block<16, false, true>);
+    else go(k_rem_block<16, false, false>);
   }
   return hipGetLastError();
 }

@@ -54,8 +54,8 @@ struct StepArgs {
 constexpr int kHeavyRow = 32;   // a row longer than this gets a whole wavefront (narrow)
 constexpr int kHubRow = 512;    // ... and one longer than this is dispatched first (wide)
 constexpr int kWideAvgRow = 24; // mean row length from which large graphs take a wave per row
-constexpr int kSourceBlockShift = 17;  // source rows per block of the remainder pass (2 MB of
-                                       // 16-B remainders: L2-resident, appnp_blocks.hip)
+constexpr int kSourceBlockRows = 1 << 17;  // source rows per block of the remainder pass
+                                           // (2 MB of 16-B remainders: L2-resident)
 
 __host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
   x += 0x9E3779B97F4A7C15ull;
