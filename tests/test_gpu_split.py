@@ -121,3 +121,18 @@ def test_split_backward_and_training_path(graphs, ahat):
     (Z * W).sum().backward()
     dref = O.appnp_backward(ahat, W.double().cpu().numpy(), 3, 0.1)
     close_fp32(H.grad.double().cpu().numpy(), dref)
+
+
+def test_split_plan_replay(graphs):
+    """The split path captured into a hipGraph (appnp_plan_*): bitwise the eager result."""
+    import ppnp_amd
+    from ppnp_amd.ops import PropagatePlan
+
+    H = _h(100, 12).to(DEV)
+    plan = PropagatePlan(graphs[0], H, K=4, alpha=0.1)
+    try:
+        assert torch.equal(plan().clone(), ppnp_amd.propagate_forward(graphs[0], H, 4, 0.1))
+        H.mul_(-0.5)  # refill in place and replay
+        assert torch.equal(plan().clone(), ppnp_amd.propagate_forward(graphs[0], H, 4, 0.1))
+    finally:
+        plan.close()
