@@ -345,8 +345,10 @@ class PartitionedAPPNP:
         if graph_fn is None:
             from .graph import Graph
 
+            # the per-rank loop runs appnp_step, which gathers whole rows: no source blocks
             graph = Graph.from_csr(indptr, indices, data, n, mode=mode, device=device,
-                                   row_lo=lo, row_hi=hi, split_local=overlap)
+                                   row_lo=lo, row_hi=hi, split_local=overlap,
+                                   source_blocks=False)
         else:
             graph = graph_fn(lo, hi, overlap)
         rows_pad = shard * layout.rows
