@@ -172,8 +172,12 @@ class MultipathComm:
 
     name = "multipath"
 
-    def __init__(self, layout: Layout, rank: int):
+    def __init__(self, layout: Layout, rank: int, widths=None):
         self.layout, self.rank = layout, rank
+        # valid columns of each column group's slab: a slab padded to a line-friendly leading
+        # dimension (25 of 32 floats) travels packed, 22 % fewer bytes over the links.  None:
+        # whole rows of the buffers (every rank's leading dimension must then agree).
+        self.widths = widths
         self.P = layout.size
         self.ri, self.ci = layout.coords(rank)
         self.backend = dist.get_backend() if dist.is_initialized() else None
@@ -220,20 +224,36 @@ class MultipathComm:
                     s2.append(("recv", b, a, pieces[tb], "full"))
         return s1, s2, len(slots), max((hi - lo for lo, hi in pieces), default=0)
 
+    def _width(self, origin: int, full) -> int:
+        if self.widths is None:
+            return full.shape[1]
+        return min(self.widths[origin // self.layout.rows], full.shape[1])
+
     def _views(self, full, shard_rows, ops, nslots, pmax):
         R = self.layout.rows
-        if nslots and (self._staging is None or self._staging.shape[1:] != (pmax, full.shape[1])
-                       or self._staging.dtype != full.dtype
-                       or self._staging.device != full.device):
-            self._staging = torch.empty(nslots, pmax, full.shape[1], dtype=full.dtype,
-                                        device=full.device)
+        # staging slot s holds a piece of origin a's slab, packed at a's width
+        slot_w = {}
+        for kind, peer, origin, (lo, hi), where in ops:
+            if where != "full":
+                slot_w[where[1]] = self._width(origin, full)
+        total = sum(pmax * w for w in slot_w.values())
+        if total and (self._staging is None or self._staging.numel() < total
+                      or self._staging.dtype != full.dtype
+                      or self._staging.device != full.device):
+            self._staging = torch.empty(total, dtype=full.dtype, device=full.device)
+        offs, off = {}, 0
+        for slot in sorted(slot_w):
+            offs[slot] = off
+            off += pmax * slot_w[slot]
         out = []
         for kind, peer, origin, (lo, hi), where in ops:
             if where == "full":
                 base = (origin % R) * shard_rows
-                t = full[base + lo:base + hi]
+                t = full[base + lo:base + hi, :self._width(origin, full)]
             else:
-                t = self._staging[where[1], :hi - lo]
+                w = slot_w[where[1]]
+                o = offs[where[1]]
+                t = self._staging[o:o + (hi - lo) * w].view(hi - lo, w)
             out.append((kind, peer, origin, t))
         return out
 
@@ -247,6 +267,10 @@ class MultipathComm:
             if host:
                 buf = t.detach().to("cpu", copy=True) if kind == "send" else torch.empty(
                     t.shape, dtype=t.dtype)
+                bufs.append((kind, t, buf))
+            elif not t.is_contiguous():  # packed: column view of a padded slab
+                buf = t.contiguous() if kind == "send" else torch.empty(
+                    t.shape, dtype=t.dtype, device=t.device)
                 bufs.append((kind, t, buf))
             fn = dist.isend if kind == "send" else dist.irecv
             if self.backend == "nccl":
@@ -360,7 +384,9 @@ class PartitionedAPPNP:
         if comm is None:
             if exchange not in ("multipath", "group"):
                 raise ValueError(f"unknown exchange {exchange!r}")
-            comm = (MultipathComm(layout, rank)
+            widths = [col_range(f, layout.cols, c)[1] - col_range(f, layout.cols, c)[0]
+                      for c in range(layout.cols)]
+            comm = (MultipathComm(layout, rank, widths)
                     if exchange == "multipath" and layout.rows > 1 and layout.cols > 1
                     else _TorchComm(layout, rank))
         step_fn = step_fn or _hip_step
