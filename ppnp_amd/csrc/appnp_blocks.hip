@@ -27,23 +27,34 @@
 namespace appnp {
 namespace {
 
-// entries of each (block, row): the row's columns are sorted, so a block is a contiguous run
+// entries of each (block, row): the row's columns are sorted, so a block is a contiguous run.
+// Also counts the off-diagonal entries within kNearRows of their row (*near: gather locality).
 __global__ __launch_bounds__(kBlock) void k_sb_count(const int32_t* __restrict__ rp,
                                                      const int32_t* __restrict__ col, int64_t rows,
-                                                     int brows, int32_t* __restrict__ cnt) {
+                                                     int64_t row_lo, int brows,
+                                                     int32_t* __restrict__ cnt,
+                                                     unsigned long long* __restrict__ near) {
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (i >= rows) return;
-  int cur = -1, c = 0;
-  for (int32_t e = rp[i]; e < rp[i + 1]; ++e) {
-    const int b = col[e] / brows;
-    if (b != cur) {
-      if (cur >= 0) cnt[(int64_t)cur * rows + i] = c;
-      cur = b;
-      c = 0;
+  unsigned long long nr = 0;
+  if (i < rows) {
+    int cur = -1, c = 0;
+    for (int32_t e = rp[i]; e < rp[i + 1]; ++e) {
+      const int32_t j = col[e];
+      const int64_t d = (int64_t)j - (row_lo + i);
+      nr += (d != 0 && d < kNearRows && d > -kNearRows) ? 1 : 0;  // the diagonal is no gather
+      const int b = j / brows;
+      if (b != cur) {
+        if (cur >= 0) cnt[(int64_t)cur * rows + i] = c;
+        cur = b;
+        c = 0;
+      }
+      ++c;
     }
-    ++c;
+    if (cur >= 0) cnt[(int64_t)cur * rows + i] = c;
   }
-  if (cur >= 0) cnt[(int64_t)cur * rows + i] = c;
+#pragma unroll
+  for (int off = 1; off < kWave; off <<= 1) nr += __shfl_xor(nr, off);
+  if ((threadIdx.x & (kWave - 1)) == 0 && nr) atomicAdd(near, nr);
 }
 
 __global__ __launch_bounds__(kBlock) void k_sb_fill(const int32_t* __restrict__ rp,
@@ -230,11 +241,12 @@ int graph_build_source_blocks(appnp_graph* g, hipStream_t s) {
       ok(hipMalloc(&g->sb_val, std::max<int64_t>(1, g->nnz_hat) * sizeof(float))) &&
       ok(hipMalloc(&cnt, std::max<int64_t>(1, cells) * sizeof(int32_t))) &&
       ok(hipMalloc(&bsum, scan_partials(cells) * sizeof(int64_t))) &&
-      ok(hipMalloc(&tot, sizeof(int64_t))) &&
+      ok(hipMalloc(&tot, 2 * sizeof(int64_t))) &&
+      ok(hipMemsetAsync(tot, 0, 2 * sizeof(int64_t), s)) &&
       ok(hipMemsetAsync(cnt, 0, std::max<int64_t>(1, cells) * sizeof(int32_t), s))) {
     if (rows > 0) {
       hipLaunchKernelGGL(k_sb_count, dim3(grid), dim3(kBlock), 0, s, g->row_ptr, g->col, rows,
-                         brows, cnt);
+                         g->row_lo, brows, cnt, reinterpret_cast<unsigned long long*>(tot + 1));
       ok(hipGetLastError());
     }
     if (rc == APPNP_OK && ok(exclusive_scan(cnt, cells, g->sb_ptr, bsum, tot, s)) && rows > 0) {
@@ -242,7 +254,11 @@ int graph_build_source_blocks(appnp_graph* g, hipStream_t s) {
                          rows, brows, g->sb_ptr, g->sb_col, g->sb_val);
       ok(hipGetLastError());
     }
-    if (rc == APPNP_OK) ok(hipStreamSynchronize(s));
+    int64_t near = 0;
+    if (rc == APPNP_OK)
+      ok(hipMemcpyAsync(&near, tot + 1, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    if (rc == APPNP_OK && ok(hipStreamSynchronize(s)))
+      g->near_frac = g->nnz_hat > 0 ? (double)near / (double)g->nnz_hat : 0.0;
   }
   if (cnt) (void)hipFree(cnt);
   if (bsum) (void)hipFree(bsum);

@@ -56,6 +56,7 @@ constexpr int kHubRow = 512;    // ... and one longer than this is dispatched fi
 constexpr int kWideAvgRow = 24; // mean row length from which large graphs take a wave per row
 constexpr int kSourceBlockRows = 1 << 17;  // source rows per block of the remainder pass
                                            // (2 MB of 16-B remainders: L2-resident)
+constexpr int kNearRows = 1 << 14;  // "near" entry: |col - row| below this (gather locality)
 
 __host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
   x += 0x9E3779B97F4A7C15ull;

@@ -41,6 +41,7 @@ struct appnp_graph {
   int32_t* sb_col = nullptr;    //   [n_sb * rows + 1], block-major (appnp_blocks.hip)
   float* sb_val = nullptr;
   int32_t n_sb = 0;
+  double near_frac = 0.0;       // off-diagonal entries within kNearRows of their row / nnz
 };
 
 struct appnp_csr;

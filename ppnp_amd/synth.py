@@ -23,6 +23,9 @@ CONFIGS = {
     "products-synth": (2449029, 61859140, 100, 10, 0.1, torch.float32),
     # power-law stand-in (SURVEY 8(d) "optionally add a Chung-Lu power-law variant")
     "products-powerlaw": (2449029, 61859140, 100, 10, 0.1, torch.float32),
+    # gather locality: communities of consecutive nodes (the order a locality-preserving
+    # relabelling gives a real graph with community structure); not a headline config
+    "products-local": (2449029, 61859140, 100, 10, 0.1, torch.float32),
     # the reference's own datasets (standardized LCC adjacency from tests/golden, which
     # tests/golden/make_golden.py took from the reference's SparseGraph.standardize)
     "cora-ml-real": (2810, 7981, 7, 10, 0.1, torch.float32),
@@ -31,12 +34,15 @@ CONFIGS = {
 REAL = {"cora-ml-real": "cora_ml", "citeseer-real": "citeseer"}
 
 SEEDS = {"pubmed-synth": 1, "ms-academic-synth": 2, "arxiv-synth": 3, "products-synth": 4,
-         "products-powerlaw": 5}
+         "products-powerlaw": 5, "products-local": 6}
 POWERLAW = {"products-powerlaw"}
+LOCAL = {"products-local"}
 DESCRIPTIONS = {name: "synthetic (uniform random graph with the dataset's node/edge counts)"
                 for name in CONFIGS}
 DESCRIPTIONS["products-powerlaw"] = ("synthetic (Chung-Lu power-law graph with the dataset's "
                                      "node/edge counts)")
+DESCRIPTIONS["products-local"] = ("synthetic (the dataset's node/edge counts; communities of "
+                                  "4096 consecutive nodes hold 90 % of the edges)")
 for _name in REAL:
     DESCRIPTIONS[_name] = "the reference's dataset (standardized LCC adjacency)"
 
@@ -91,6 +97,35 @@ def chung_lu_graph_device(n: int, m: int, seed: int, exponent: float = 3.2,
     return indptr.to(torch.int32), col
 
 
+def community_graph_device(n: int, m: int, seed: int, block: int = 4096, p_in: float = 0.9,
+                           device="cuda"):
+    """Graph with gather locality: the source of each of the m pairs is uniform; with
+    probability p_in its destination is uniform inside the source's community (``block``
+    consecutive node ids), otherwise uniform over all nodes.  Then the same symmetrise /
+    de-duplicate / no-self-loop steps as ``uniform_graph_device``.  A community's rows of an
+    F = 100 fp32 Z are 1.6 MB, so the rows a wave front gathers stay in L2."""
+    g = torch.Generator(device=device).manual_seed(seed)
+    src = torch.randint(0, n, (m,), device=device, generator=g, dtype=torch.int64)
+    far = torch.randint(0, n, (m,), device=device, generator=g, dtype=torch.int64)
+    base = torch.div(src, block, rounding_mode="floor") * block
+    near = (base + torch.randint(0, block, (m,), device=device, generator=g)).clamp_(max=n - 1)
+    inside = torch.rand(m, device=device, generator=g) < p_in
+    dst = torch.where(inside, near, far)
+    del far, base, near, inside
+    keep = src != dst
+    src, dst = src[keep], dst[keep]
+    key = torch.cat([src * n + dst, dst * n + src])
+    del src, dst, keep
+    key = torch.unique(key, sorted=True)
+    row = torch.div(key, n, rounding_mode="floor")
+    col = (key - row * n).to(torch.int32)
+    del key
+    counts = torch.bincount(row, minlength=n)
+    indptr = torch.zeros(n + 1, dtype=torch.int64, device=device)
+    indptr[1:] = torch.cumsum(counts, 0)
+    return indptr.to(torch.int32), col
+
+
 def real_graph(name: str, device="cuda"):
     """CSR of a dataset the reference ships, standardized as its SparseGraph does."""
     import os
@@ -110,6 +145,8 @@ def graph_for(workload: str, device="cuda"):
     n, m = CONFIGS[workload][:2]
     if workload in POWERLAW:
         return chung_lu_graph_device(n, m, SEEDS[workload], device=device)
+    if workload in LOCAL:
+        return community_graph_device(n, m, SEEDS[workload], device=device)
     return uniform_graph_device(n, m, SEEDS.get(workload, 0), device=device)
 
 

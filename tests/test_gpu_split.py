@@ -136,3 +136,20 @@ def test_split_plan_replay(graphs):
         assert torch.equal(plan().clone(), ppnp_amd.propagate_forward(graphs[0], H, 4, 0.1))
     finally:
         plan.close()
+
+
+def test_split_point_follows_gather_locality(graphs):
+    """Split rows only where gathers miss L2: a uniform graph splits F = 100 at 96; a graph whose
+    edges stay within communities of consecutive nodes keeps whole rows (its last line is
+    mostly an L2 hit); bf16 and F = 128 never split."""
+    import ppnp_amd
+    from ppnp_amd import synth
+
+    assert graphs[0].split_point(100) == 96
+    assert graphs[0].split_point(97) == 96 and graphs[0].split_point(36) == 32
+    assert graphs[0].split_point(128) == 0 and graphs[0].split_point(101) == 0
+    assert graphs[0].split_point(100, torch.bfloat16) == 0
+    assert graphs[1].split_point(100) == 0  # built without source blocks
+    ip, ix = synth.community_graph_device(N, 1_500_000, 7, device=DEV)
+    local = ppnp_amd.Graph.from_csr(ip, ix, None, N, device=DEV)
+    assert local.split_point(100) == 0

@@ -30,4 +30,5 @@ tools/gpu_session.sh \
  "w_arxiv::200::$B --workload arxiv-synth" \
  "w_cora::200::$B --workload cora-ml" \
  "w_powerlaw::200::$B --workload products-powerlaw" \
+ "w_local::200::$B --workload products-local" \
  "w_bf16::200::$B --dtype bf16"
