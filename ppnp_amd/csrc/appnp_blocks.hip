@@ -168,9 +168,9 @@ __global__ __launch_bounds__(kBlock) void k_rem_block(StepArgs a, const int32_t*
     for (int u = 0; u < U; ++u) {
       c[u] = 0;
       w[u] = 0.0f;
-      if (e + u < end) {
-        c[u] = ld_nt<int32_t>(bcol + e + u);
-        w[u] = ld_nt<float>(bval + e + u);
+      if (e + u < end) {  // cached: neighbouring lanes' runs share lines (non-temporal: -1 %)
+        c[u] = bcol[e + u];
+        w[u] = bval[e + u];
       }
     }
     f32x4 v[U];

@@ -125,7 +125,7 @@ int64_t split_point(const appnp_graph* g, int64_t f, int dtype, int V) {
   // graphs with gather locality keep whole rows: their last line is mostly an L2 hit, cheaper
   // than the remainder pass (products-local, 88 % near entries: 4.0 ms whole rows, 3.7 ms for
   // the 3-line main part alone, 8.5 ms split).  Uniform products-synth: 1.3 % near.
-  if (g->near_frac > kSplitMaxNear) return 0;
+  if (g->near_frac > kSplitMaxNear && enabled != 2) return 0;  // APPNP_SPLIT=2: regardless
   const int64_t r = f % 32;
   return (r >= 1 && r <= 4) ? f - r : 0;
 }
