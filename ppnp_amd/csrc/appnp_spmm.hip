@@ -362,15 +362,8 @@ hipError_t launch_wide(int G, dim3 grid, const StepArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <typename T, int V, int EPI, bool TAIL>
-hipError_t launch_g(int G, bool wide, int uw, dim3 grid, const StepArgs& a, hipStream_t s) {
-  constexpr int UN = 4;  // entries in flight per row (narrow)
-  if (wide) {
-    if (uw == 8) return launch_wide<T, V, EPI, TAIL, 8>(G, grid, a, s);
-    if (uw == 4) return launch_wide<T, V, EPI, TAIL, 4>(G, grid, a, s);
-    if (uw == 2) return launch_wide<T, V, EPI, TAIL, 2>(G, grid, a, s);
-    return launch_wide<T, V, EPI, TAIL, 1>(G, grid, a, s);
-  }
+template <typename T, int V, int EPI, bool TAIL, int UN>
+hipError_t launch_narrow(int G, dim3 grid, const StepArgs& a, hipStream_t s) {
   const dim3 block(kBlock);
   switch (G) {
     case 1: hipLaunchKernelGGL((k_step_narrow<T, V, 1, EPI, UN, TAIL>), grid, block, 0, s, a); break;
@@ -382,20 +375,37 @@ hipError_t launch_g(int G, bool wide, int uw, dim3 grid, const StepArgs& a, hipS
   return hipGetLastError();
 }
 
+// entries in flight: uw per sub-group of the wide kernels, un per row of the narrow ones
+template <typename T, int V, int EPI, bool TAIL>
+hipError_t launch_g(int G, bool wide, int uw, int un, dim3 grid, const StepArgs& a,
+                    hipStream_t s) {
+  if (wide) {
+    if (uw == 8) return launch_wide<T, V, EPI, TAIL, 8>(G, grid, a, s);
+    if (uw == 4) return launch_wide<T, V, EPI, TAIL, 4>(G, grid, a, s);
+    if (uw == 2) return launch_wide<T, V, EPI, TAIL, 2>(G, grid, a, s);
+    return launch_wide<T, V, EPI, TAIL, 1>(G, grid, a, s);
+  }
+  if constexpr (V == 1) {
+    if (un == 8) return launch_narrow<T, V, EPI, TAIL, 8>(G, grid, a, s);
+  }
+  return launch_narrow<T, V, EPI, TAIL, 4>(G, grid, a, s);
+  return hipGetLastError();
+}
+
 template <typename T, int EPI>
-hipError_t launch_v(int V, int G, bool wide, int uw, dim3 grid, const StepArgs& a,
+hipError_t launch_v(int V, int G, bool wide, int uw, int un, dim3 grid, const StepArgs& a,
                     hipStream_t s) {
   const bool tail = (a.f % V) != 0;
   switch (V) {
-    case 1: return launch_g<T, 1, EPI, false>(G, wide, uw, grid, a, s);
-    case 2: return tail ? launch_g<T, 2, EPI, true>(G, wide, uw, grid, a, s)
-                        : launch_g<T, 2, EPI, false>(G, wide, uw, grid, a, s);
-    case 4: return tail ? launch_g<T, 4, EPI, true>(G, wide, uw, grid, a, s)
-                        : launch_g<T, 4, EPI, false>(G, wide, uw, grid, a, s);
+    case 1: return launch_g<T, 1, EPI, false>(G, wide, uw, un, grid, a, s);
+    case 2: return tail ? launch_g<T, 2, EPI, true>(G, wide, uw, un, grid, a, s)
+                        : launch_g<T, 2, EPI, false>(G, wide, uw, un, grid, a, s);
+    case 4: return tail ? launch_g<T, 4, EPI, true>(G, wide, uw, un, grid, a, s)
+                        : launch_g<T, 4, EPI, false>(G, wide, uw, un, grid, a, s);
     case 8:
       if constexpr (sizeof(T) == 2)
-        return tail ? launch_g<T, 8, EPI, true>(G, wide, uw, grid, a, s)
-                    : launch_g<T, 8, EPI, false>(G, wide, uw, grid, a, s);
+        return tail ? launch_g<T, 8, EPI, true>(G, wide, uw, un, grid, a, s)
+                    : launch_g<T, 8, EPI, false>(G, wide, uw, un, grid, a, s);
       return hipErrorInvalidValue;
     default: return hipErrorInvalidValue;
   }
@@ -486,19 +496,24 @@ hipError_t launch_step(int dtype, int epi, int V, const StepArgs& a_in, hipStrea
   static const int uw_env = env_int("APPNP_UW", -1);  // measurement override (1, 2, 4, 8)
   const int uw = uw_env > 0 ? uw_env : (latency && heavy_rows) ? 8 : (!latency && long_rows) ? 2 : 1;
   // cache policy of the streams (StepArgs::nt); APPNP_NT overrides for measurement
+  // entries in flight per row of the narrow kernels: 8 in the latency regime, where a row's
+  // dependent rounds set the launch time (pubmed-synth 5.77 -> 5.24 us, cora-sized uniform
+  // 6.01 -> 5.45 us per iteration; tools/sweep_uw.sh), else 4
+  static const int un_env = env_int("APPNP_UN", -1);  // measurement override (4, 8)
+  const int un = un_env > 0 ? un_env : latency ? 8 : 4;
   static const int nt_env = env_int("APPNP_NT", -1);
   a.nt = nt_env >= 0 ? nt_env : (latency ? 0 : 1);
   if (dtype == 0) {
     switch (epi) {
-      case EPI_FWD: return launch_v<float, EPI_FWD>(V, G, wide, uw, grid, a, s);
-      case EPI_BWD: return launch_v<float, EPI_BWD>(V, G, wide, uw, grid, a, s);
-      case EPI_PARTIAL: return launch_v<float, EPI_PARTIAL>(V, G, wide, uw, grid, a, s);
-      case EPI_FINISH: return launch_v<float, EPI_FINISH>(V, G, wide, uw, grid, a, s);
+      case EPI_FWD: return launch_v<float, EPI_FWD>(V, G, wide, uw, un, grid, a, s);
+      case EPI_BWD: return launch_v<float, EPI_BWD>(V, G, wide, uw, un, grid, a, s);
+      case EPI_PARTIAL: return launch_v<float, EPI_PARTIAL>(V, G, wide, uw, un, grid, a, s);
+      case EPI_FINISH: return launch_v<float, EPI_FINISH>(V, G, wide, uw, un, grid, a, s);
     }
   } else {
     switch (epi) {
-      case EPI_FWD: return launch_v<uint16_t, EPI_FWD>(V, G, wide, uw, grid, a, s);
-      case EPI_BWD: return launch_v<uint16_t, EPI_BWD>(V, G, wide, uw, grid, a, s);
+      case EPI_FWD: return launch_v<uint16_t, EPI_FWD>(V, G, wide, uw, un, grid, a, s);
+      case EPI_BWD: return launch_v<uint16_t, EPI_BWD>(V, G, wide, uw, un, grid, a, s);
     }
   }
   return hipErrorInvalidValue;
