@@ -174,7 +174,11 @@ int appnp_propagate_split_point(const appnp_graph* g, int64_t f, int dtype, int6
  *   hash of (seed, k, i, j) >= p_drop * 2^24, and scales kept edges by 1/(1-p_drop).
  *   p_drop = 0 is eval mode (the reference's semantics).
  *   ws: appnp_workspace_bytes() bytes (may be NULL when that is 0).
- * One fused kernel launch per iteration.  Requires a full (non-partitioned) graph.
+ * One fused kernel launch per iteration.  With split rows (appnp_propagate_split_point > 0)
+ * an iteration is that launch on the first fs columns plus the remainder pass (one launch per
+ * source block), and H is first copied into the workspace's split layout.  All launches are
+ * stream-ordered on `stream`; nothing is allocated or synchronised.  Requires a full
+ * (non-partitioned) graph.
  */
 int appnp_propagate(const appnp_graph* g, const void* H, int64_t ld_h, void* Z, int64_t ld_z,
                     int64_t f, int dtype, int K, float alpha, float p_drop, uint64_t seed,
