@@ -412,6 +412,14 @@ class PartitionedAPPNP:
         if K == 0:
             self.out = self.H[:, :w]
             return self.out
+        if R == 1 and self.step_fn is _hip_step:
+            # column layout: this rank holds every row of its slab, so the K iterations are one
+            # appnp_propagate call (no per-iteration host work between the launches)
+            from .ops import propagate_forward
+
+            self.out = propagate_forward(self.graph, self.H[:, :w], K, self.alpha, self.p_drop,
+                                         self.seed, out=self.bufs[1][:, :w])
+            return self.out
         # Z_0 = H: the full Z_0 needs every row shard of H (iteration 0 gathers from it)
         cur = self.bufs[0]
         cur[lo:hi].copy_(self.H)
