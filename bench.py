@@ -286,7 +286,9 @@ def main():
     # gather line-request rate: every nonzero gathers one row of Z_k; with
     # split rows only the fs main columns are gathered (whole lines), the rest run the
     # L2-blocked remainder pass (appnp_blocks.hip)
-    fs = graph.split_point(F_local, dtype) if not distributed and K >= 2 else 0
+    # (single GPU, or a column layout, whose ranks call appnp_propagate on their slab)
+    whole = not distributed or runner.layout.rows == 1
+    fs = graph.split_point(F_local, dtype) if whole and K >= 2 else 0
     ld_l = pdist.line_ld(F_local, s)
     lines_per_row = (fs * s // 128 if fs else
                      1 if ld_l * s <= 128 else -(-(F_local * s) // 128))
@@ -345,7 +347,8 @@ def main():
                 "ceiling_source": "tools/gather_probe.hip, profiles/r1_gather_probe.txt",
             },
             "kernel": ("k_step_wide (one launch per iteration)" if not fs else
-                       f"k_step_wide on columns [0, {fs}) + k_rem_block x {-(-n // (1 << 17))} "
+                       f"k_step_wide on columns [0, {fs}) of the slab + k_rem_block x "
+                       f"{-(-n // (1 << 17))} "
                        f"(remainder columns, L2-blocked) per iteration; times are per iteration"),
             "bytes_per_launch": b_iter,
             "avg_launch_ms": avg_launch_ms,

@@ -369,10 +369,14 @@ class PartitionedAPPNP:
         if graph_fn is None:
             from .graph import Graph
 
-            # the per-rank loop runs appnp_step, which gathers whole rows: no source blocks
+            # source blocks only where the rank's loop is one appnp_propagate call (column
+            # layout) on a slab whose rows split (fp32, width 32q + r, r <= 4); appnp_step
+            # gathers whole rows
+            split = (layout.rows == 1 and H.dtype == torch.float32 and n > (1 << 16)
+                     and 32 < width <= 256 and width % 32 in (1, 2, 3, 4))
             graph = Graph.from_csr(indptr, indices, data, n, mode=mode, device=device,
                                    row_lo=lo, row_hi=hi, split_local=overlap,
-                                   source_blocks=False)
+                                   source_blocks=split)
         else:
             graph = graph_fn(lo, hi, overlap)
         rows_pad = shard * layout.rows
