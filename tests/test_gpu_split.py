@@ -153,3 +153,22 @@ def test_split_point_follows_gather_locality(graphs):
     ip, ix = synth.community_graph_device(N, 1_500_000, 7, device=DEV)
     local = ppnp_amd.Graph.from_csr(ip, ix, None, N, device=DEV)
     assert local.split_point(100) == 0
+
+
+@pytest.mark.parametrize("mode", ["sym", "rw"])
+def test_split_weighted_and_rw(adj, mode):
+    """Edge weights travel with the source-blocked copy (bval), and 'rw' (not symmetric) uses
+    the same path."""
+    import ppnp_amd
+
+    w = adj.copy()
+    rng = np.random.default_rng(13)
+    w.data = rng.uniform(0.5, 2.0, size=w.nnz).astype(np.float32)
+    w = ((w + w.T) * 0.5).tocsr()
+    w.sort_indices()
+    G = ppnp_amd.Graph.from_scipy(w, mode=mode, device=DEV)
+    assert G.split_point(100) == 96
+    H = _h(100, 14)
+    Z = ppnp_amd.propagate_forward(G, H.to(DEV), 3, 0.15, p_drop=0.2, seed=5)
+    ref = O.appnp_propagate(O.calc_a_hat(w, mode), H.numpy(), 3, 0.15, p_drop=0.2, seed=5)
+    close_fp32(Z.double().cpu().numpy(), ref)
