@@ -385,7 +385,7 @@ hipError_t launch_g(int G, bool wide, int uw, int un, dim3 grid, const StepArgs&
     if (uw == 2) return launch_wide<T, V, EPI, TAIL, 2>(G, grid, a, s);
     return launch_wide<T, V, EPI, TAIL, 1>(G, grid, a, s);
   }
-  if constexpr (V == 1) {
+  if constexpr (V <= 2) {
     if (un == 8) return launch_narrow<T, V, EPI, TAIL, 8>(G, grid, a, s);
   }
   return launch_narrow<T, V, EPI, TAIL, 4>(G, grid, a, s);
@@ -449,19 +449,23 @@ hipError_t launch_step(int dtype, int epi, int V, const StepArgs& a_in, hipStrea
   // reduction -- and a wavefront per row only when the graph has hub rows.
   constexpr int64_t kLatencyRows = 1 << 16;
   const bool latency = a.n_rows <= kLatencyRows;
-  if (latency) {
+  const int v_max = V;  // widest vector every operand allows (pick_vec)
+  const bool heavy_rows = a.heavy && a.n_heavy > 0;
+  if (latency && !heavy_rows) {
     int v = 1;
     while (v < V && (int64_t)64 * v < a.f) v <<= 1;
     V = v;
   }
+  // latency regime with hub rows (a wavefront per row): the widest vector, so a row needs the
+  // fewest lanes and the most sub-groups walk the longest row at once (Cora-ML 5.94 -> 5.21 us
+  // per iteration with V = 4 instead of 1; Citeseer 4.06 -> 3.89 us with V = 2)
   static const int v_env = env_int("APPNP_VEC", -1);  // measurement override (<= pick_vec's)
-  if (v_env > 0 && v_env <= V) V = v_env;
+  if (v_env > 0 && v_env <= v_max) V = v_env;
   const int G = lanes_for(V);
   // Bandwidth regime: a wavefront per row also for narrow F once rows are long on average
   // (products-synth slabs of 4-25 features, 51.5 entries a row: 6-10 % faster than G-lane
   // rows; uniform and power-law; arxiv-synth, 14.8 a row: G-lane rows 20-50 % faster).
   const bool long_rows = a.nnz >= (int64_t)kWideAvgRow * a.n_rows;
-  const bool heavy_rows = a.heavy && a.n_heavy > 0;
   static const int wide_env = env_int("APPNP_WIDE", -1);  // measurement override
   const bool wide = wide_env >= 0 ? wide_env != 0
                                   : (G >= 16 || (latency && heavy_rows) || (!latency && long_rows));
