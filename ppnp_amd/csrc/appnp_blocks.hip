@@ -95,9 +95,18 @@ __device__ __forceinline__ void rem_finish(const StepArgs& a, int64_t i, f32x4 a
   if constexpr (!LAST) {
     static_cast<f32x4*>(a.aux)[i] = acc;
   } else {
-    // H rows are 16-B aligned with ld_h >= roundup(f, 4): the 16 B at H_rem stay in the row
-    f32x4 h = *reinterpret_cast<const f32x4*>(static_cast<const float*>(a.h) + i * a.ld_h);
+    // H rows are 16-B aligned with ld_h >= roundup(f, 4): the 16 B at H_rem stay inside the
+    // row's storage, except possibly on the buffer's last row (read exactly nv there)
     const int nv = a.f;
+    const float* hp = static_cast<const float*>(a.h) + i * a.ld_h;
+    f32x4 h = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    if (nv == 4 || i + 1 < a.n_rows) {
+      h = *reinterpret_cast<const f32x4*>(hp);
+    } else {
+      h.x = hp[0];
+      if (nv > 1) h.y = hp[1];
+      if (nv > 2) h.z = hp[2];
+    }
     const float y[4] = {fmaf(a.alpha, h.x, a.scale * acc.x),
                         fmaf(a.alpha, nv > 1 ? h.y : 0.0f, a.scale * acc.y),
                         fmaf(a.alpha, nv > 2 ? h.z : 0.0f, a.scale * acc.z),
@@ -158,7 +167,7 @@ __global__ __launch_bounds__(kBlock) void k_rem_block(StepArgs a, const int32_t*
   }
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= a.n_rows) return;
-  if (a.n_hub && a.row_ptr[i + 1] - a.row_ptr[i] > kHubRow) return;  // a trailing block's
+  if (a.n_hub && a.row_ptr[i + 1] - a.row_ptr[i] > kHubRow) return;  // hub: trailing blocks
   f32x4 acc = FIRST ? f32x4{0.0f, 0.0f, 0.0f, 0.0f} : r[i];
   const int32_t end = ptr[i + 1];
   for (int32_t e = ptr[i]; e < end; e += U) {
@@ -201,14 +210,24 @@ __global__ __launch_bounds__(kBlock) void k_split_copy(const float* __restrict__
        t += (int64_t)gridDim.x * kBlock) {
     const int64_t row = t / pieces;
     const int q = (int)(t - row * pieces);
-    f32x4 v = ld_nt<f32x4>(h + row * ld_h + 4 * q);
+    const float* p = h + row * ld_h + 4 * q;
     if (q < fs / 4) {
-      *reinterpret_cast<f32x4*>(main + row * fs + 4 * q) = v;
+      *reinterpret_cast<f32x4*>(main + row * fs + 4 * q) = ld_nt<f32x4>(p);
     } else {
+      // the remainder piece: a full 16-B read stays inside the row's storage except possibly
+      // on the buffer's last row, which reads exactly its nv valid columns
       const int nv = f - fs;
-      if (nv < 4) v.w = 0.0f;
-      if (nv < 3) v.z = 0.0f;
-      if (nv < 2) v.y = 0.0f;
+      f32x4 v = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+      if (nv == 4 || row + 1 < n) {
+        v = ld_nt<f32x4>(p);
+        if (nv < 4) v.w = 0.0f;
+        if (nv < 3) v.z = 0.0f;
+        if (nv < 2) v.y = 0.0f;
+      } else {
+        v.x = p[0];
+        if (nv > 1) v.y = p[1];
+        if (nv > 2) v.z = p[2];
+      }
       *reinterpret_cast<f32x4*>(rem + row * 4) = v;
     }
   }

@@ -172,3 +172,21 @@ def test_split_weighted_and_rw(adj, mode):
     Z = ppnp_amd.propagate_forward(G, H.to(DEV), 3, 0.15, p_drop=0.2, seed=5)
     ref = O.appnp_propagate(O.calc_a_hat(w, mode), H.numpy(), 3, 0.15, p_drop=0.2, seed=5)
     close_fp32(Z.double().cpu().numpy(), ref)
+
+
+def test_split_exact_size_last_row(graphs, ahat):
+    """H and Z whose storage ends exactly at the last valid column (ld 100, F = 97): the split
+    copy and the remainder epilogue read and write only the valid columns of that row."""
+    import ppnp_amd
+
+    f, ld = 97, 100
+    H = _h(f, 15)
+    hs = torch.zeros((N - 1) * ld + f, device=DEV)
+    Hv = hs.as_strided((N, f), (ld, 1))
+    Hv.copy_(H.to(DEV))
+    zs = torch.full(((N - 1) * ld + f,), 3.0, device=DEV)
+    Zv = zs.as_strided((N, f), (ld, 1))
+    ppnp_amd.propagate_forward(graphs[0], Hv, 3, 0.1, out=Zv)
+    close_fp32(Zv.double().cpu().numpy(), O.appnp_propagate(ahat, H.numpy(), 3, 0.1))
+    pad = zs[: (N - 1) * ld].view(N - 1, ld)[:, f:]
+    assert bool((pad == 3.0).all())  # the gaps between rows are untouched
