@@ -187,7 +187,8 @@ int appnp_propagate(const appnp_graph* g, const void* H, int64_t ld_h, void* Z, 
 /*
  * dH = J^T dZ for the map H -> Z of appnp_propagate with the same (K, alpha, p_drop, seed).
  * Uses A_hat^T: A_hat itself for 'sym' on an undirected graph, otherwise the transpose built
- * at creation with APPNP_GRAPH_TRANSPOSE; APPNP_ENOTSUP if neither is available.
+ * at creation with APPNP_GRAPH_TRANSPOSE; APPNP_ENOTSUP if neither is available.  On a
+ * self-adjoint A_hat it uses the same column split as appnp_propagate.
  */
 int appnp_propagate_bwd(const appnp_graph* g, const void* dZ, int64_t ld_dz, void* dH,
                         int64_t ld_dh, int64_t f, int dtype, int K, float alpha, float p_drop,

@@ -90,10 +90,26 @@ __global__ __launch_bounds__(kBlock) void k_sb_fill(const int32_t* __restrict__ 
 // a.out / a.ld_out, a.f = nv valid columns: 4 into the next Z_rem, 1-4 into Z's last columns).
 // (A single launch keeping every row's sum in registers while all threads walk the blocks
 // measured slower: threads drift apart and the blocks they gather from no longer fit L2.)
-template <bool FIRST, bool LAST>
+template <int EPI, bool FIRST, bool LAST>
 __device__ __forceinline__ void rem_finish(const StepArgs& a, int64_t i, f32x4 acc) {
   if constexpr (!LAST) {
     static_cast<f32x4*>(a.aux)[i] = acc;
+  } else if constexpr (EPI == EPI_BWD) {
+    // adjoint: G_k = (1-alpha) R into the next remainder buffer (none at k = 0), and
+    // dH[:, fs:f] += alpha' G_k (exactly nv columns)
+    const float y[4] = {a.scale * acc.x, a.scale * acc.y, a.scale * acc.z, a.scale * acc.w};
+    if (a.out)
+      static_cast<f32x4*>(a.out)[i] = f32x4{y[0], y[1], y[2], y[3]};
+    const int nv = a.f;
+    float* d = a.rem_dh + i * a.ld_rem_dh;
+    if (nv == 4) {
+      f32x4 v = *reinterpret_cast<f32x4*>(d);
+      v = f32x4{fmaf(a.alpha, y[0], v.x), fmaf(a.alpha, y[1], v.y), fmaf(a.alpha, y[2], v.z),
+                fmaf(a.alpha, y[3], v.w)};
+      *reinterpret_cast<f32x4*>(d) = v;
+    } else {
+      for (int v = 0; v < nv; ++v) d[v] = fmaf(a.alpha, y[v], d[v]);
+    }
   } else {
     // H rows are 16-B aligned with ld_h >= roundup(f, 4): the 16 B at H_rem stay inside the
     // row's storage, except possibly on the buffer's last row (read exactly nv there)
@@ -124,7 +140,7 @@ __device__ __forceinline__ void rem_finish(const StepArgs& a, int64_t i, f32x4 a
 // all, listed in a.hub; the light threads skip them), a wavefront each -- its lanes stride
 // over the row's entries of the block and a fixed butterfly adds them -- so a power-law hub
 // does not serialise one thread while the launch waits.
-template <int U, bool FIRST, bool LAST>
+template <int U, int EPI, bool FIRST, bool LAST>
 __global__ __launch_bounds__(kBlock) void k_rem_block(StepArgs a, const int32_t* __restrict__ ptr,
                                                       const int32_t* __restrict__ bcol,
                                                       const float* __restrict__ bval) {
@@ -160,7 +176,7 @@ __global__ __launch_bounds__(kBlock) void k_rem_block(StepArgs a, const int32_t*
           const f32x4 p = r[i];
           acc = f32x4{p.x + acc.x, p.y + acc.y, p.z + acc.z, p.w + acc.w};
         }
-        rem_finish<FIRST, LAST>(a, i, acc);
+        rem_finish<EPI, FIRST, LAST>(a, i, acc);
       }
     }
     return;
@@ -195,7 +211,7 @@ __global__ __launch_bounds__(kBlock) void k_rem_block(StepArgs a, const int32_t*
       acc.w = fmaf(wu, v[u].w, acc.w);
     }
   }
-  rem_finish<FIRST, LAST>(a, i, acc);
+  rem_finish<EPI, FIRST, LAST>(a, i, acc);
 }
 
 // H [n, ld_h] -> the split layout: main [n, fs] (whole lines per row) and rem [n, 4]
@@ -298,18 +314,25 @@ int graph_build_source_blocks(appnp_graph* g, hipStream_t s) {
 // launch per block in block order, the last one applying the epilogue (k_rem_block).
 // a: the iteration's StepArgs (dropout key, row_lo, n_rows, scale, alpha); z_rem [n, 4];
 // acc [rows, 4] scratch (may be `out` itself when out is a Z_rem buffer); h_rem = H + fs;
-// out / ld_out / nv: where the nv valid columns of Z_{k+1} go.
+// out / ld_out / nv: where the nv valid columns of Z_{k+1} go.  epi = EPI_BWD (adjoint): h_rem
+// / ld_h are dH's remainder columns, accumulated into; out (G_k's remainder) may be null.
 // Entries in flight per thread: 16 (products-synth per iteration: 1 -> 1.6 ms, 8 -> 1.4 ms,
 // 16 0.05 ms less; tools/sweep_split.sh).  Blocks of 2^17 source rows measured best
 // (2^16, 96k, 160k, 192k and 2^18 rows: +0.01-0.3 ms).
-hipError_t launch_remainder(const appnp_graph* g, const StepArgs& a_in, const float* z_rem,
-                            float* acc, const float* h_rem, int64_t ld_h, float* out,
-                            int64_t ld_out, int nv, hipStream_t s) {
+hipError_t launch_remainder(const appnp_graph* g, const StepArgs& a_in, int epi,
+                            const float* z_rem, float* acc, const float* h_rem, int64_t ld_h,
+                            float* out, int64_t ld_out, int nv, hipStream_t s) {
   StepArgs a = a_in;
   a.zin = z_rem;
   a.aux = acc;
-  a.h = h_rem;
-  a.ld_h = ld_h;
+  if (epi == EPI_BWD) {  // h_rem / ld_h: dH's remainder columns, accumulated into
+    a.h = nullptr;
+    a.rem_dh = const_cast<float*>(h_rem);
+    a.ld_rem_dh = ld_h;
+  } else {
+    a.h = h_rem;
+    a.ld_h = ld_h;
+  }
   a.out = out;
   a.ld_out = ld_out;
   a.f = nv;
@@ -328,10 +351,17 @@ hipError_t launch_remainder(const appnp_graph* g, const StepArgs& a_in, const fl
     auto go = [&](auto kern) {
       hipLaunchKernelGGL(kern, grid, block, 0, s, a, p, g->sb_col, g->sb_val);
     };
-    if (first && last) go(k_rem_block<16, true, true>);
-    else if (first) go(k_rem_block<16, true, false>);
-    else if (last) go(k_rem_block<16, false, true>);
-    else go(k_rem_block<16, false, false>);
+    if (epi == EPI_BWD) {
+      if (first && last) go(k_rem_block<16, EPI_BWD, true, true>);
+      else if (first) go(k_rem_block<16, EPI_BWD, true, false>);
+      else if (last) go(k_rem_block<16, EPI_BWD, false, true>);
+      else go(k_rem_block<16, EPI_BWD, false, false>);
+    } else {
+      if (first && last) go(k_rem_block<16, EPI_FWD, true, true>);
+      else if (first) go(k_rem_block<16, EPI_FWD, true, false>);
+      else if (last) go(k_rem_block<16, EPI_FWD, false, true>);
+      else go(k_rem_block<16, EPI_FWD, false, false>);
+    }
   }
   return hipGetLastError();
 }

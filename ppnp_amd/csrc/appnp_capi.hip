@@ -166,9 +166,49 @@ int propagate_split(const appnp_graph* g, const StepArgs& a0, const void* H, int
     rc = dev_err(appnp::launch_step(APPNP_F32, appnp::EPI_FWD, 4, am, s));
     if (rc) break;
     set_drop(ar, p_drop, seed, k);
-    rc = dev_err(appnp::launch_remainder(g, ar, rem_of(cur), rem_of(dst), h + fs, ld_h,
+    rc = dev_err(appnp::launch_remainder(g, ar, appnp::EPI_FWD, rem_of(cur), rem_of(dst),
+                                         h + fs, ld_h,
                                          last ? z + fs : rem_of(dst), last ? ld_z : 4,
                                          last ? (int)(f - fs) : 4, s));
+    cur = dst;
+  }
+  return rc;
+}
+
+// The adjoint loop in the split layout: the same two independent chains as propagate_split,
+// run backwards (G_K = dZ, G_k = (1-alpha) M_k^T G_{k+1}, dH += alpha' G_k), for a
+// self-adjoint A_hat.  dH = alpha dZ is set by the caller.
+int propagate_bwd_split(const appnp_graph* g, const StepArgs& a0, const void* dZ, int64_t ld_dz,
+                        void* dH, int64_t ld_dh, int64_t fs, int K, float alpha, float p_drop,
+                        uint64_t seed, char* ws, int64_t main_b, int64_t buf_b, hipStream_t s) {
+  const int64_t n = a0.n_rows, f = a0.f;
+  char* bufs[2] = {ws, ws + buf_b};
+  auto main_of = [&](int i) { return reinterpret_cast<float*>(bufs[i]); };
+  auto rem_of = [&](int i) { return reinterpret_cast<float*>(bufs[i] + main_b); };
+  int rc = dev_err(appnp::launch_split_copy(static_cast<const float*>(dZ), ld_dz, n, f, fs,
+                                            main_of(0), rem_of(0), s));
+  StepArgs am = a0, ar = a0;  // main / remainder chain
+  am.f = (int32_t)fs;
+  am.aux = dH;
+  am.ld_aux = ld_dh;
+  am.ld_in = fs;
+  am.ld_out = fs;
+  float* dh_rem = static_cast<float*>(dH) + fs;
+  int cur = 0;
+  for (int k = K - 1; k >= 0 && !rc; --k) {
+    const int dst = cur ^ 1;
+    const float a_k = k >= 1 ? alpha : 1.0f;
+    set_drop(am, p_drop, seed, k);
+    am.alpha = a_k;
+    am.zin = main_of(cur);
+    am.out = k == 0 ? nullptr : main_of(dst);
+    rc = dev_err(appnp::launch_step(APPNP_F32, appnp::EPI_BWD, 4, am, s));
+    if (rc) break;
+    set_drop(ar, p_drop, seed, k);
+    ar.alpha = a_k;
+    rc = dev_err(appnp::launch_remainder(g, ar, appnp::EPI_BWD, rem_of(cur), rem_of(dst), dh_rem,
+                                         ld_dh, k == 0 ? nullptr : rem_of(dst), 4,
+                                         (int)(f - fs), s));
     cur = dst;
   }
   return rc;
@@ -377,6 +417,7 @@ int appnp_propagate_bwd(const appnp_graph* g, const void* dZ, int64_t ld_dz, voi
   const int64_t ld_w = line_ld(f, dtype);
   const int64_t buf = n * ld_w * es;
   const int nbuf = K >= 3 ? 2 : (K == 2 ? 1 : 0);
+  void* const ws_orig = ws;
   if (nbuf > 0) {
     if (!ws) return APPNP_EINVAL;
     const uintptr_t base = reinterpret_cast<uintptr_t>(ws);
@@ -394,6 +435,16 @@ int appnp_propagate_bwd(const appnp_graph* g, const void* dZ, int64_t ld_dz, voi
   // dH += alpha G_k (k >= 1) / dH += G_0.
   rc = dev_err(appnp::launch_scale_rows(dtype, dZ, ld_dz, dH, ld_dh, n, f, alpha, s));
   if (rc) return rc;
+  // split rows (self-adjoint A_hat: the source-blocked copy of A_hat is that of A_hat^T)
+  const int64_t fs = (self_adjoint && K >= 2) ? split_point(g, f, dtype, V) : 0;
+  int64_t main_b = 0, buf_b = 0;
+  if (fs > 0) {
+    main_b = (n * fs * 4 + 255) / 256 * 256;
+    buf_b = (main_b + n * 16 + 255) / 256 * 256;
+    const size_t used = (size_t)(reinterpret_cast<uintptr_t>(ws) -
+                                 reinterpret_cast<uintptr_t>(ws_orig));
+    if (ws_bytes < used + 2 * (size_t)buf_b) main_b = 0;  // too small: whole rows
+  }
   StepArgs a = base_args(g, f, alpha);
   if (!self_adjoint) {
     a.row_ptr = g->t_row_ptr;
@@ -405,6 +456,9 @@ int appnp_propagate_bwd(const appnp_graph* g, const void* dZ, int64_t ld_dz, voi
     a.n_hub = g->t_n_hub;
   }
   a.tkey = 1;  // entry (j, i) of A_hat^T carries the mask of forward edge (i, j)
+  if (fs > 0 && main_b > 0)
+    return propagate_bwd_split(g, a, dZ, ld_dz, dH, ld_dh, fs, K, alpha, p_drop, seed,
+                               static_cast<char*>(ws), main_b, buf_b, s);
   a.aux = dH;
   a.ld_aux = ld_dh;
   const void* src = dZ;

@@ -49,6 +49,8 @@ struct StepArgs {
   int32_t nt;              // cache policy of the streams (set by launch_step): bit 0 col/val,
                            // bit 1 H, bit 2 Zout -- non-temporal, so they do not evict the
                            // gathered rows of Zin from the Infinity Cache
+  float* rem_dh;           // remainder pass, adjoint: dH's remainder columns (rows x ld_rem_dh)
+  int64_t ld_rem_dh;
 };
 
 constexpr int kHeavyRow = 32;   // a row longer than this gets a whole wavefront (narrow)

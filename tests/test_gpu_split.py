@@ -190,3 +190,19 @@ def test_split_exact_size_last_row(graphs, ahat):
     close_fp32(Zv.double().cpu().numpy(), O.appnp_propagate(ahat, H.numpy(), 3, 0.1))
     pad = zs[: (N - 1) * ld].view(N - 1, ld)[:, f:]
     assert bool((pad == 3.0).all())  # the gaps between rows are untouched
+
+
+@pytest.mark.parametrize("f,K,p", [(100, 2, 0.0), (97, 3, 0.0), (36, 3, 0.25), (100, 4, 0.3)])
+def test_split_adjoint_matches_oracle(graphs, ahat, f, K, p):
+    """appnp_propagate_bwd in the split layout (self-adjoint A_hat), against the float64
+    adjoint of the oracle, with the transposed dropout keys."""
+    import ppnp_amd
+
+    dZ = _h(f, 20 + f + K)
+    dH = ppnp_amd.propagate_backward(graphs[0], dZ.to(DEV), K, 0.1, p_drop=p, seed=9)
+    ref = O.appnp_backward(ahat, dZ.numpy(), K, 0.1, p_drop=p, seed=9)
+    close_fp32(dH.double().cpu().numpy(), ref)
+    plain = ppnp_amd.propagate_backward(graphs[1], dZ.to(DEV), K, 0.1, p_drop=p, seed=9)
+    close_fp32(dH.double().cpu().numpy(), plain.double().cpu().numpy())
+    again = ppnp_amd.propagate_backward(graphs[0], dZ.to(DEV), K, 0.1, p_drop=p, seed=9)
+    assert torch.equal(dH, again)
