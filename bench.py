@@ -295,6 +295,7 @@ def main():
     lines = nnz_local * lines_per_row + (8 * nnz_local + 3 * rows_local * ld_l * s) / 128
     line_rate = lines / (avg_launch_ms * 1e-3) / 1e9
     value = n * F * K * args.steps / wall
+    rows_per_s = n * K * args.steps / wall  # also N*K/t
     parallelism = ((f"rows{runner.layout.rows}xcols{runner.layout.cols}"
                     + ("-overlap" if runner.overlap else "")
                     + (f"-{runner.exchange}" if runner.layout.rows > 1 and runner.layout.cols > 1
@@ -310,6 +311,7 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": wall * 1e3 / args.steps,
+        "propagated_rows_per_s": rows_per_s,
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
