@@ -123,7 +123,7 @@ int64_t split_point(const appnp_graph* g, int64_t f, int dtype, int V) {
   if (!enabled || !g->sb_ptr || dtype != APPNP_F32 || V != 4) return 0;
   if (g->n <= (1 << 16) || f <= 32 || f > 256) return 0;
   // graphs with gather locality keep whole rows: their last line is mostly an L2 hit, cheaper
-  // than the remainder pass (products-local, 88 % near entries: 4.0 ms whole rows, 3.7 ms for
+  // than the remainder pass (products-local, ~90 % near entries: 4.0 ms whole rows, 3.7 ms for
   // the 3-line main part alone, 8.5 ms split).  Uniform products-synth: 1.3 % near.
   if (g->near_frac > kSplitMaxNear && enabled != 2) return 0;  // APPNP_SPLIT=2: regardless
   const int64_t r = f % 32;
