@@ -92,8 +92,8 @@ int main(int argc, char** argv) {
   CHECK(hipMemset(table, 0, max_table));
   std::vector<int> h(n_idx);
   const int64_t table_mb[] = {16, 64, 128, 192, 256, 384, 1024, 4096};
-  const int row_bytes[] = {64, 128, 256, 400, 512};
-  printf("table_MB row_B  ms   gathered_GB/s  lines_GB/s(128B)\n");
+  const int row_bytes[] = {64, 128, 256, 384, 400, 512};
+  printf("table_MB row_B  ms   gathered_GB/s  (nt: the same with non-temporal loads)\n");
   uint64_t s = 88172645463325252ull;
   for (int rb : row_bytes) {
     for (int64_t tmb : table_mb) {
@@ -115,6 +115,8 @@ int main(int argc, char** argv) {
                   ms_nt = run<8, true>(table, ld4, lanes, idx, n_idx, sink, blocks); break;
         case 256: ms = run<16, false>(table, ld4, lanes, idx, n_idx, sink, blocks);
                   ms_nt = run<16, true>(table, ld4, lanes, idx, n_idx, sink, blocks); break;
+        case 384: ms = run<32, false>(table, ld4, lanes, idx, n_idx, sink, blocks);
+                  ms_nt = run<32, true>(table, ld4, lanes, idx, n_idx, sink, blocks); break;
         case 400: ms = run<32, false>(table, ld4, lanes, idx, n_idx, sink, blocks);
                   ms_nt = run<32, true>(table, ld4, lanes, idx, n_idx, sink, blocks); break;
         case 512: ms = run<32, false>(table, ld4, lanes, idx, n_idx, sink, blocks);
