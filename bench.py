@@ -52,8 +52,9 @@ def parse():
                    help="override the workload's storage dtype (non-headline variants)")
     p.add_argument("--features", type=int, default=None,
                    help="override the workload's feature width F (non-headline variants)")
-    p.add_argument("--cpu-iters", type=int, default=10,
-                   help="iterations of the CPU baseline sample (0 disables it)")
+    p.add_argument("--cpu-iters", type=int, default=None,
+                   help="iterations of the CPU baseline sample (default K: its Z_K is then the "
+                        "parity reference of the GPU result; 0 disables it)")
     p.add_argument("--layout", default="auto",
                    help="multi-GPU layout: auto | row | col | RxC (row groups x column groups)")
     p.add_argument("--emulate", default=None, metavar="P:r",
@@ -85,27 +86,72 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(graph, H, K, alpha, iters):
-    """Time the oracle's CPU torch.sparse.mm APPNP loop on the same operator and H."""
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_threads() -> tuple[int, int]:
+    """(threads to use, CPUs this process may run on).  BASELINE.md asks for every core; on the
+    GPU box the process's share is what OMP_NUM_THREADS names (16 of a much larger machine, whose
+    full count os.cpu_count() reports), so that bounds it."""
+    visible = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    share = int(os.environ.get("OMP_NUM_THREADS") or 0) or visible
+    return max(1, min(visible, share)), visible
+
+
+def cpu_baseline(graph, H, K, alpha, iters, adj=None):
+    """Time the oracle's CPU torch.sparse.mm APPNP loop on the same operator and H (SURVEY.md
+    8(d) CPU baseline (i)); return (the JSON object, Z of the CPU loop).  For N <= 20k also time
+    the reference's as-shipped PPNP path, compute_ppr + dense Pi @ H (helpers.py:68-71,
+    model.py:63; baseline (ii))."""
     from oracle import ppnp_oracle as O
 
+    threads, visible = cpu_threads()
+    torch.set_num_threads(threads)
     rp, col, val, _ = graph.csr()
     a_t = torch.sparse_csr_tensor(rp.cpu().long(), col.cpu().long(), val.cpu(),
                                   size=(graph.n, graph.n))
     Hc = H.float().cpu()
-    threads = torch.get_num_threads()
     t0 = time.perf_counter()
-    O.appnp_propagate_torch_cpu(a_t, Hc, iters, alpha)
+    Zc = O.appnp_propagate_torch_cpu(a_t, Hc, iters, alpha)
     dt = time.perf_counter() - t0
     n, f = Hc.shape
-    return {
+    res = {
         "value": n * f * iters / dt,
         "unit": "node-feats/s",
         "cores": threads,
+        "threads": threads,
+        "cpus_visible": visible,
+        "cpu_model": cpu_model(),
         "kind": "port",
         "sample": f"full graph, {iters} of K={K} iterations, torch.sparse.mm fp32 CSR "
                   f"(oracle/ppnp_oracle.py appnp_propagate_torch_cpu), {dt:.2f} s",
     }
+    if adj is not None and n <= 20000:
+        import numpy as np
+
+        t0 = time.perf_counter()
+        Pi = O.compute_ppr(adj, alpha)
+        t_ppr = time.perf_counter() - t0
+        Hn = Hc.double().numpy()
+        t0 = time.perf_counter()
+        _ = np.asarray(Pi, dtype=np.float32) @ Hn.astype(np.float32)
+        t_mm = time.perf_counter() - t0
+        res["ppnp_as_shipped"] = {
+            "compute_ppr_s": t_ppr,
+            "dense_pi_h_s": t_mm,
+            "value": n * f / (t_ppr + t_mm),
+            "unit": "node-feats/s (one exact propagation, K -> infinity)",
+            "sample": "oracle compute_ppr (helpers.py:68-71: dense fp64 inverse) + fp32 Pi @ H",
+        }
+    return res, Zc
 
 
 def tune_layouts(cands, indptr, indices, n, H, K, alpha, dev, ctl_dev, reps=2):
@@ -226,7 +272,8 @@ def main():
         nnz_total = int(nnz_t.item())
     else:
         t1 = time.perf_counter()
-        graph = ppnp_amd.Graph.from_csr(indptr, indices, None, n, mode="sym", device=dev)
+        graph = ppnp_amd.Graph.from_csr(indptr, indices, None, n, mode="sym", device=dev,
+                                        features=F, dtype=dtype)
         torch.cuda.synchronize()
         t_build = time.perf_counter() - t1
         Z = torch.empty(n, ld, dtype=dtype, device=dev)[:, :F]
@@ -235,6 +282,7 @@ def main():
             from ppnp_amd.ops import PropagatePlan
 
             plan = PropagatePlan(graph, H, K, alpha)
+            Z = plan.Z
 
             def run():
                 plan()
@@ -246,6 +294,16 @@ def main():
         stream = torch.cuda.current_stream(dev)
         F_local = F
         nnz_total = graph.nnz_hat
+    adj_small = None
+    if n <= 20000 and world == 1:  # the as-shipped PPNP leg of the CPU baseline needs A
+        import numpy as np
+        import scipy.sparse as sp
+
+        ip_c, ix_c = indptr.cpu().numpy(), indices.cpu().numpy()
+        adj_small = sp.csr_matrix((np.ones(len(ix_c), dtype=np.float32), ix_c, ip_c),
+                                  shape=(n, n))
+    if distributed:
+        ref_csr = (indptr, indices)  # rank-0 style verification of the partitioned result
     del indices
     if rank == 0:
         log(f"[bench] {args.workload}: N={n} nnz_hat={nnz_total} F={F} K={K} dtype={dtype} "
@@ -275,6 +333,30 @@ def main():
         t = torch.tensor([wall, dev_ms], dtype=torch.float64, device=ctl_dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         wall, dev_ms = float(t[0]), float(t[1])
+
+    # parity of the timed result: at N > 1 every rank compares its block of Z_K with a
+    # single-GPU appnp_propagate of the whole graph on its own device (max over ranks), so a
+    # wrong exchange fails loudly instead of printing a throughput
+    dist_parity = None
+    if distributed and not args.emulate:
+        Zblk = runner.out
+        ip_r, ix_r = ref_csr
+        Gref = ppnp_amd.Graph.from_csr(ip_r, ix_r, None, n, mode="sym", device=dev)
+        Zref = ppnp_amd.propagate_forward(Gref, H, K, alpha)
+        blk = Zref[runner.lo:runner.hi, runner.f_lo:runner.f_hi]
+        err = float((Zblk.double() - blk.double()).abs().max()) if blk.numel() else 0.0
+        ref_max = float(Zref.abs().max())
+        e = torch.tensor([err, ref_max], dtype=torch.float64, device=ctl_dev)
+        if world > 1:
+            torch.distributed.all_reduce(e, op=torch.distributed.ReduceOp.MAX)
+        err, ref_max = float(e[0]), float(e[1])
+        tol = 1e-5 * ref_max + 1e-6
+        dist_parity = {"max_abs_err": err, "tol": tol, "max_abs_ref": ref_max,
+                       "ok": err <= tol,
+                       "reference": "single-GPU appnp_propagate of the whole graph, per rank"}
+        del Gref, Zref, blk, ref_csr
+        if not dist_parity["ok"]:
+            log(f"[bench] PARITY FAILURE of the partitioned result: {dist_parity}")
 
     s = 2 if dtype == torch.bfloat16 else 4
     rows_local = graph.rows
@@ -354,12 +436,42 @@ def main():
                        f"(remainder columns, L2-blocked) per iteration; times are per iteration"),
             "bytes_per_launch": b_iter,
             "avg_launch_ms": avg_launch_ms,
+            # the access-pattern bound: every nonzero gathers a random row of Z,
+            # i.e. `lines_per_row` 128-B line requests (3 for a split F = 100 fp32 row), plus the
+            # streamed lines, at the chip's measured random-line rate; the L2-resident remainder
+            # pass is left out, so this is a lower bound on the iteration time
+            "ceiling": {
+                "ms_per_iter": lines / (GATHER_LINE_CEILING * 1e9) * 1e3,
+                "frac": b_iter / (lines / (GATHER_LINE_CEILING * 1e9)) / 1e9 / HBM_PEAK_GBS,
+                "lines_per_nonzero": lines_per_row,
+                "basis": f"{lines:.4g} line requests per iteration at the {GATHER_LINE_CEILING} "
+                         "G lines/s random-gather rate of tools/gather_probe.hip",
+            },
+            "note": "a uniform random graph gathers whole cache lines per nonzero, so the "
+                    "compulsory-byte fraction is capped at ceiling.frac; 60 % of the "
+                    "compulsory-byte roofline is out of reach for it on one GPU",
         },
     }
     if autotune is not None:
         res["config"]["autotune_ms_per_step"] = autotune
-    if world == 1 and args.cpu_iters > 0:
-        res["cpu_baseline"] = cpu_baseline(graph, H, K, alpha, args.cpu_iters)
+    if dist_parity is not None:
+        res["parity"] = dist_parity
+    cpu_iters = K if args.cpu_iters is None else args.cpu_iters
+    if world == 1 and cpu_iters > 0 and not distributed:
+        res["cpu_baseline"], Zc = cpu_baseline(graph, H, K, alpha, cpu_iters, adj_small)
+        if cpu_iters == K:
+            # value parity of the timed GPU result against the oracle's fp32 CPU loop on the
+            # same A_hat and H; fp32 bar of the tests: 1e-5 max|Z_ref| + 1e-6
+            err = float((Z.float().cpu() - Zc).abs().max())
+            ref_max = float(Zc.abs().max())
+            tol = 1e-5 * ref_max + 1e-6
+            if dtype == torch.bfloat16:
+                tol = 2e-2 * ref_max  # bf16 storage bar
+            res["parity"] = {"max_abs_err": err, "tol": tol, "max_abs_ref": ref_max,
+                             "ok": err <= tol,
+                             "reference": "oracle fp32 torch.sparse.mm CPU loop, same A_hat "
+                                          "and H, all K iterations"}
+        del Zc
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:

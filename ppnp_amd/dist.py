@@ -518,15 +518,21 @@ def candidate_layouts(world: int, f: int, n: int = 0, nnz_hat: int = 0, elem_byt
     which only an xGMI measurement can price.  Candidates that do not
     fit (``fits``) are dropped; if none does, the row-heaviest layout that fits is used."""
     first = choose_layout(world, n, f, nnz_hat, elem_bytes, mem_bytes)
+    row = Layout(world, 1)
+    # the north_star's design -- a pure row partition, all-gather overlapped with the local
+    # product -- is always timed when it fits, so the scaling run measures it next to the rest
+    row_cand = ([(row, True, "group")]
+                if world >= 2 and fits(row, n, f, nnz_hat, elem_bytes, True, mem_bytes) else [])
     if first.rows > 1:  # row groups forced by size: overlap the exchange, try both routes
-        return [(first, True, "multipath"), (first, True, "group")] if first.cols > 1 else [
-            (first, True, "group")]
+        cands = ([(first, True, "multipath"), (first, True, "group")] if first.cols > 1 else
+                 [(first, True, "group")])
+        return cands + [c for c in row_cand if c[0] != first]
     cands = [(first, False, "group")]
     if world >= 8 and world % 2 == 0 and f >= world // 2:
         two = Layout(2, world // 2)
         if fits(two, n, f, nnz_hat, elem_bytes, True, mem_bytes):
             cands += [(two, True, "multipath"), (two, True, "group")]
-    return cands
+    return cands + [c for c in row_cand if c[0] != first]
 
 
 def choose_layout(world: int, n: int, f: int, nnz: int, elem_bytes: int = 4,

@@ -9,6 +9,8 @@ A_hat there (fp64 arithmetic, fp32 storage, bit-identical to float32 of the refe
 from __future__ import annotations
 
 import ctypes as C
+import itertools
+import weakref
 
 import numpy as np
 import torch
@@ -24,14 +26,36 @@ def _ptr(t):
     return C.c_void_p(t.data_ptr()) if t is not None and t.numel() > 0 else None
 
 
+def splits_rows(n: int, features: int, dtype=torch.float32) -> bool:
+    """Whether appnp_propagate would take the split-row path for this shape on a graph built
+    with source blocks (appnp_capi.hip split_point): fp32 rows of F = 32q + r features with
+    1 <= r <= 4, 32 < F <= 256, above the latency regime (n > 2^16 rows)."""
+    return (dtype == torch.float32 and n > (1 << 16) and 32 < features <= 256
+            and features % 32 in (1, 2, 3, 4))
+
+
 class Graph:
     """A_hat = calc_A_hat(adj, mode) held on one GPU (all rows, or rows [row_lo, row_hi)).
 
     Build it with :meth:`from_scipy` (host CSR) or :meth:`from_csr` (torch CSR arrays).
     """
 
+    # live graphs by integer key: the torch.library ops (ops.py) take the key, since a custom
+    # op's schema cannot carry a Python object
+    _registry: "weakref.WeakValueDictionary[int, Graph]" = weakref.WeakValueDictionary()
+    _next_key = itertools.count(1)
+
+    @classmethod
+    def lookup(cls, key: int) -> "Graph":
+        g = cls._registry.get(int(key))
+        if g is None or g._h is None:
+            raise RuntimeError(f"ppnp_amd: graph key {key} is not a live Graph")
+        return g
+
     def __init__(self, handle, device):
         self._h = handle
+        self.key = next(Graph._next_key)
+        Graph._registry[self.key] = self
         self.device = torch.device(device)
         lib = _lib.load()
         n, lo, hi, nnz = C.c_int64(), C.c_int64(), C.c_int64(), C.c_int64()
@@ -48,13 +72,17 @@ class Graph:
     # -- construction ---------------------------------------------------------------------
     @classmethod
     def from_csr(cls, indptr, indices, data, n, mode="sym", device=None, row_lo=0,
-                 row_hi=None, split_local=False, transpose=False, source_blocks=None):
+                 row_hi=None, split_local=False, transpose=False, source_blocks=None,
+                 features=None, dtype=torch.float32):
         """indptr/indices (int32) and optional data (fp32) of A; tensors or arrays.
         ``transpose=True`` also builds A_hat^T when A_hat is not symmetric (rw mode or a
         directed graph), which the backward needs.  ``source_blocks`` keeps the copy of A_hat
         blocked by source rows that lets fp32 rows of F = 32q + r (r <= 4) features gather q
-        cache lines instead of q + 1 (APPNP_GRAPH_SOURCE_BLOCKS); default: full graphs above
-        the latency regime (n > 65536)."""
+        cache lines instead of q + 1 (APPNP_GRAPH_SOURCE_BLOCKS).  Default: only when the
+        caller names a feature width ``features`` (and storage ``dtype``) that takes that path
+        on a full graph above the latency regime (``splits_rows``) -- the copy costs about as
+        much memory as the CSR itself, so it is never built on speculation.  The build is
+        best-effort: if the copy does not fit, the graph keeps whole-row gathers."""
         if mode not in _lib.NORM:
             raise ValueError(f"mode must be 'sym' or 'rw', got {mode!r}")
         device = torch.device(device if device is not None else "cuda")
@@ -76,7 +104,8 @@ class Graph:
         nnz = int(ix.numel())
         row_hi = n if row_hi is None else int(row_hi)
         if source_blocks is None:
-            source_blocks = n > (1 << 16) and int(row_lo) == 0 and row_hi == n
+            source_blocks = (features is not None and int(row_lo) == 0 and row_hi == n
+                             and splits_rows(n, int(features), dtype))
         flags = ((_lib.GRAPH_TRANSPOSE if transpose else 0)
                  | (_lib.GRAPH_SOURCE_BLOCKS if source_blocks else 0))
         lib = _lib.load()

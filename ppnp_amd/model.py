@@ -126,22 +126,50 @@ class APPNP(nn.Module):
         self.register_buffer("adj_indptr", torch.from_numpy(a.indptr.astype(np.int32)))
         self.register_buffer("adj_indices", torch.from_numpy(a.indices.astype(np.int32)))
         self.register_buffer("adj_data", torch.from_numpy(a.data.astype(np.float32)))
+        self.n_classes = int(n_classes)
         self.alpha = float(alpha)
         self.K = int(K)
         self.mode = mode
         self.edge_drop = float(edge_drop)
         self.prop_dtype = dtype
+        self.ppr_topk = None  # batch-main.py:113-117 sparsification of the lazy ``ppr``
         self._graph = None
+        self._ppr = None  # (device, topk, dense Pi) built on first access of ``ppr``
         self._memo = None  # (key, Z_K) of the last no-grad eval-mode propagation
         self.memo_hits = 0
 
     def graph(self) -> Graph:
         dev = self.adj_indptr.device
         if self._graph is None or self._graph.device != dev:
+            # the propagation carries n_classes columns: the source-blocked copy of A_hat is
+            # built only when that width takes the split-row path (graph.splits_rows)
             self._graph = Graph.from_csr(self.adj_indptr, self.adj_indices, self.adj_data,
                                          self.n_nodes, mode=self.mode, device=dev,
-                                         transpose=True)
+                                         transpose=True, features=self.n_classes,
+                                         dtype=self.prop_dtype)
         return self._graph
+
+    # K of the series behind ``ppr``: (1-alpha)^K below fp32 resolution of the rows
+    PPR_TOL = 1e-7
+
+    @property
+    def ppr(self) -> torch.Tensor:
+        """The dense PPR matrix Pi = alpha (I - (1-alpha) A_hat)^-1 (helpers.py:68-71), for
+        callers that index the reference model's ``ppr`` buffer directly -- batch-main.py:140
+        ``model.ppr[idx_batch]``.  Built lazily on the graph's device from the K-step series
+        of one-hot columns (ppr.ppr_rows; K chosen so (1-alpha)^K <= PPR_TOL), with the
+        column-wise top-k of batch-main.py:115-116 applied when ``ppr_topk`` is set.  N x N:
+        small graphs only, exactly as in the reference."""
+        from .ppr import batch_topk_quirk, dense_ppr
+
+        g = self.graph()
+        key = (g.device, self.ppr_topk)
+        if self._ppr is None or self._ppr[0] != key:
+            K = int(math.ceil(math.log(self.PPR_TOL) / math.log(1.0 - self.alpha)))
+            P = (batch_topk_quirk(g, self.ppr_topk, K, self.alpha) if self.ppr_topk
+                 else dense_ppr(g, K, self.alpha))
+            self._ppr = (key, P)
+        return self._ppr[1]
 
     def get_norm(self):
         return sum((torch.sum(param ** 2) for param in self._reg_params))
@@ -155,20 +183,31 @@ class APPNP(nn.Module):
     def _memo_key(self, X):
         """Identity of everything Z_K depends on, for deterministic (eval, no-grad) calls:
         main.py evaluates the stopping and validation sets with two forwards of the same X
-        and weights (main.py:138, 145); the second reuses the first's Z_K.  Any in-place
-        change (optimizer step, load_state_dict, edited X) bumps a tensor version."""
+        and weights (main.py:138, 145); the second reuses the first's Z_K.
+
+        The key holds the tensors themselves (strong references) and their versions: a hit
+        needs the SAME tensor objects (``is``), unchanged in place (an optimizer step,
+        load_state_dict or an edited X bumps ``_version``).  A new X that the caching
+        allocator happens to place at a just-freed address is a different object, so it can
+        never match a stale entry."""
         if self.training or torch.is_grad_enabled():
             return None
         xs = (X.indptr, X.indices, X.data) if isinstance(X, SparseFeatures) else (X,)
-        state = [*xs, *self.parameters(), *self.buffers()]
-        return (tuple((t.data_ptr(), t._version, tuple(t.shape)) for t in state),
-                self.K, self.alpha, self.mode, self.prop_dtype)
+        state = (*xs, *self.parameters(), *self.buffers())
+        return (state, tuple(t._version for t in state), self.K, self.alpha, self.mode,
+                self.prop_dtype)
+
+    @staticmethod
+    def _memo_match(a, b) -> bool:
+        return (a is not None and b is not None and len(a[0]) == len(b[0])
+                and all(x is y for x, y in zip(a[0], b[0])) and a[1:] == b[1:])
 
     def forward(self, X, idx=None, ppr=None):
         """X: dense tensor (as the reference) or ppnp_amd.SparseFeatures (CSR on the GPU)."""
         if idx is not None:
             key = self._memo_key(X)
-            if key is not None and self._memo is not None and self._memo[0] == key:
+            if key is not None and self._memo is not None and self._memo_match(self._memo[0],
+                                                                               key):
                 self.memo_hits += 1
                 return self._memo[1][idx]
             Z = self.propagate(_encode(self.encoder, X, self.training))

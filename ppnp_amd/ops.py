@@ -87,22 +87,52 @@ def propagate_backward(graph: Graph, dZ: torch.Tensor, K: int, alpha: float, p_d
     return dH
 
 
-class _Propagate(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, H, graph, K, alpha, p_drop, seed):
-        ctx.graph, ctx.K, ctx.alpha, ctx.p_drop, ctx.seed = graph, K, alpha, p_drop, seed
-        return propagate_forward(graph, H.contiguous(), K, alpha, p_drop, seed)
+# ---- torch.library registration ---------------------------------------------------------
+# ``ppnp_amd::propagate`` / ``ppnp_amd::propagate_bwd`` are real dispatcher ops: torch.compile
+# traces through them without a graph break (fake kernels give the output metadata), and
+# autograd is registered on the op itself.  A custom op cannot take a Python object, so the
+# graph crosses the dispatcher as the integer key Graph.key (graph.py registry).
+# Call sites served: the three propagations per epoch of main.py:121, 138, 145.
 
-    @staticmethod
-    def backward(ctx, dZ):
-        dH = propagate_backward(ctx.graph, dZ, ctx.K, ctx.alpha, ctx.p_drop, ctx.seed)
-        return dH, None, None, None, None, None
+
+@torch.library.custom_op("ppnp_amd::propagate", mutates_args=(), device_types="cuda")
+def _propagate_op(H: torch.Tensor, graph_key: int, K: int, alpha: float, p_drop: float,
+                  seed: int) -> torch.Tensor:
+    return propagate_forward(Graph.lookup(graph_key), H.contiguous(), K, alpha, p_drop, seed)
+
+
+@_propagate_op.register_fake
+def _(H, graph_key, K, alpha, p_drop, seed):
+    return torch.empty(H.shape, dtype=H.dtype, device=H.device)
+
+
+@torch.library.custom_op("ppnp_amd::propagate_bwd", mutates_args=(), device_types="cuda")
+def _propagate_bwd_op(dZ: torch.Tensor, graph_key: int, K: int, alpha: float, p_drop: float,
+                      seed: int) -> torch.Tensor:
+    return propagate_backward(Graph.lookup(graph_key), dZ, K, alpha, p_drop, seed)
+
+
+@_propagate_bwd_op.register_fake
+def _(dZ, graph_key, K, alpha, p_drop, seed):
+    return torch.empty(dZ.shape, dtype=dZ.dtype, device=dZ.device)
+
+
+def _propagate_setup(ctx, inputs, output):
+    ctx.args = inputs[1:]
+
+
+def _propagate_grad(ctx, dZ):
+    return (torch.ops.ppnp_amd.propagate_bwd(dZ, *ctx.args), None, None, None, None, None)
+
+
+_propagate_op.register_autograd(_propagate_grad, setup_context=_propagate_setup)
 
 
 def propagate(graph: Graph, H: torch.Tensor, K: int = 10, alpha: float = 0.1,
               p_drop: float = 0.0, seed: int = 0) -> torch.Tensor:
-    """Differentiable APPNP propagation Z_K(H) on the GPU."""
-    return _Propagate.apply(H, graph, int(K), float(alpha), float(p_drop), int(seed))
+    """Differentiable APPNP propagation Z_K(H) on the GPU (the ``ppnp_amd::propagate`` op)."""
+    return torch.ops.ppnp_amd.propagate(H, graph.key, int(K), float(alpha), float(p_drop),
+                                        int(seed) & (2**63 - 1))
 
 
 def step(graph: Graph, Zin: torch.Tensor, H: torch.Tensor, out: torch.Tensor, k: int,

@@ -61,18 +61,25 @@ def ppr_rows(graph: Graph, idx, K: int = 10, alpha: float = 0.1, topk: int | Non
     return rows
 
 
+def dense_ppr(graph: Graph, K: int = 10, alpha: float = 0.1, chunk: int = 1024) -> torch.Tensor:
+    """All of Pi (N x N fp32), row chunks of ``ppr_rows``: the truncated series of
+    compute_ppr (helpers.py:68-71).  Small graphs only (materialises N x N)."""
+    n = graph.n
+    if n * n > 2**31:
+        raise ValueError("dense_ppr materialises N x N: N too large")
+    P = torch.empty(n, n, dtype=torch.float32, device=graph.device)
+    for s in range(0, n, chunk):
+        idx = torch.arange(s, min(n, s + chunk), device=graph.device)
+        P[s:s + len(idx)] = ppr_rows(graph, idx, K, alpha)
+    return P
+
+
 def batch_topk_quirk(graph: Graph, topk: int, K: int = 10, alpha: float = 0.1,
                      chunk: int = 1024) -> torch.Tensor:
     """Dense sparsified Pi exactly as batch-main.py:115-116 builds it:
     ``thresh, _ = ppr.topk(k, axis=-1); ppr[ppr < thresh[:, -1]] = 0`` (column-wise top-k
     through broadcasting).  Small graphs only (materialises N x N)."""
-    n = graph.n
-    if n * n > 2**31:
-        raise ValueError("batch_topk_quirk materialises N x N: N too large")
-    P = torch.empty(n, n, dtype=torch.float32, device=graph.device)
-    for s in range(0, n, chunk):
-        idx = torch.arange(s, min(n, s + chunk), device=graph.device)
-        P[s:s + len(idx)] = ppr_rows(graph, idx, K, alpha)
+    P = dense_ppr(graph, K, alpha, chunk)
     thresh, _ = P.topk(topk, dim=-1)
     P[P < thresh[:, -1]] = 0
     return P

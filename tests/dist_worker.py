@@ -1,9 +1,9 @@
 #!/usr/bin/env python
 """End-to-end check of the multi-GPU path on real HIP kernels.
 
-    torchrun --nproc-per-node P --master-addr 127.0.0.1 tools/dist_check.py --layout row|col|RxC
+    torchrun --nproc-per-node P --master-addr 127.0.0.1 tests/dist_worker.py --layout row|col|RxC
         [--overlap] [--exchange multipath|group] [--n 60000] [--m 400000] [--f 20] [--K 10]
-        [--p-drop 0.0]
+        [--p-drop 0.0] [--workload arxiv-synth] [--oracle]
 
 Every rank runs its share (ppnp_amd.dist.PartitionedAPPNP) and compares its block of Z_K with
 the single-GPU propagation of the whole graph computed on its own device.  Backend: RCCL when
@@ -33,6 +33,12 @@ def main():
     p.add_argument("--K", type=int, default=10)
     p.add_argument("--alpha", type=float, default=0.1)
     p.add_argument("--p-drop", type=float, default=0.0)
+    p.add_argument("--workload", default=None,
+                   help="a ppnp_amd.synth.CONFIGS graph (its n, m, F, K, alpha, seed) instead of "
+                        "--n/--m/--f/--K/--alpha")
+    p.add_argument("--oracle", action="store_true",
+                   help="compare with the float64 CPU oracle (oracle/ppnp_oracle.py) instead of "
+                        "the single-GPU HIP propagation")
     a = p.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -50,23 +56,40 @@ def main():
     else:
         dist.init_process_group(backend)
     rank = dist.get_rank()
-    indptr, indices = synth.uniform_graph_device(a.n, a.m, 7, device=dev)
+    if a.workload:
+        a.n, a.m, a.f, a.K, a.alpha, _ = synth.CONFIGS[a.workload]
+        indptr, indices = synth.graph_for(a.workload, device=dev)
+    else:
+        indptr, indices = synth.uniform_graph_device(a.n, a.m, 7, device=dev)
     H = synth.features(a.n, a.f, device=dev, seed=1)
     runner = pdist.PartitionedAPPNP.create(indptr, indices, a.n, H, a.K, a.alpha, dev,
                                            layout=layout, overlap=a.overlap,
                                            p_drop=a.p_drop, seed=5, exchange=a.exchange)
     Z = runner.run()
     torch.cuda.synchronize()
-    G = ppnp_amd.Graph.from_csr(indptr, indices, None, a.n, device=dev)
-    ref = ppnp_amd.propagate_forward(G, H, a.K, a.alpha, p_drop=a.p_drop, seed=5)
+    if a.oracle:
+        import numpy as np
+        import scipy.sparse as sp
+
+        from oracle import ppnp_oracle as O
+
+        adj = sp.csr_matrix((np.ones(indices.numel(), dtype=np.float32), indices.cpu().numpy(),
+                             indptr.cpu().numpy()), shape=(a.n, a.n))
+        ref = torch.from_numpy(O.appnp_propagate(O.calc_a_hat(adj, "sym"),
+                                                 H.double().cpu().numpy(), a.K, a.alpha,
+                                                 p_drop=a.p_drop, seed=5)).to(dev)
+    else:
+        G = ppnp_amd.Graph.from_csr(indptr, indices, None, a.n, device=dev)
+        ref = ppnp_amd.propagate_forward(G, H, a.K, a.alpha, p_drop=a.p_drop, seed=5)
     block = ref[runner.lo:runner.hi, runner.f_lo:runner.f_hi]
     err = (Z.double() - block.double()).abs().max().item() if block.numel() else 0.0
     tol = 1e-5 * ref.abs().max().item() + 1e-6
     ok = err <= tol
-    print(f"[dist_check] rank {rank}/{world} backend={dist.get_backend()} layout={layout} "
+    print(f"[dist_worker] rank {rank}/{world} backend={dist.get_backend()} layout={layout} "
           f"overlap={runner.overlap} exchange={runner.exchange} rows [{runner.lo},{runner.hi}) "
           f"cols [{runner.f_lo},"
-          f"{runner.f_hi}) max err {err:.3e} tol {tol:.3e} -> {'OK' if ok else 'FAIL'}",
+          f"{runner.f_hi}) reference={'oracle' if a.oracle else 'hip'} max err {err:.3e} "
+          f"tol {tol:.3e} -> {'OK' if ok else 'FAIL'}",
           flush=True)
     flag = torch.tensor([0 if ok else 1], dtype=torch.int64,
                         device=dev if dist.get_backend() == "nccl" else "cpu")

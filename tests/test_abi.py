@@ -78,3 +78,21 @@ def test_no_cpu_fallback_when_library_missing(tmp_path, monkeypatch):
     with pytest.raises(ImportError):
         _lib.load()
     importlib.reload(_lib)
+
+
+def test_torch_library_ops_registered_with_fake_kernels():
+    """ppnp_amd::propagate / propagate_bwd are dispatcher ops with fake (meta) kernels, so
+    torch.compile can trace them; shapes propagate without touching a device."""
+    import torch
+
+    import ppnp_amd  # noqa: F401  (registers the ops)
+
+    for name in ("propagate", "propagate_bwd"):
+        op = getattr(torch.ops.ppnp_amd, name)
+        H = torch.empty(7, 3, device="meta")
+        Z = op(H, 1, 10, 0.1, 0.0, 0)
+        assert Z.shape == (7, 3) and Z.device.type == "meta" and Z.dtype == H.dtype
+    with pytest.raises(RuntimeError):
+        from ppnp_amd.graph import Graph
+
+        Graph.lookup(10**9)  # not a live graph: loud, no fallback

@@ -1,0 +1,151 @@
+"""GPU parity on BASELINE.json's configs at their full sizes.
+
+Every check runs the HIP path through the C ABI on the synthetic graph the bench uses and
+compares the WHOLE Z_K with an oracle computed on the CPU from the same A and H:
+
+* config 2, pubmed-synth (19,717 x 3, K = 10, fp32) and config 4, arxiv-synth (169,343 x 128,
+  K = 10, fp32): the float64 oracle (oracle/ppnp_oracle.py appnp_propagate, the K-step series
+  of helpers.py:58-71), fp32 bar max|Z - Z_ref| <= 1e-5 max|Z_ref| + 1e-6;
+* config 3, ms-academic-synth (18,333 x 15, K = 20, alpha = 0.2, bf16 storage): the bf16 bar
+  <= 2e-2 max|Z_ref| with >= 98 % argmax agreement;
+* config 5, products-synth (2,449,029 x 100, K = 10, fp32; 126 M nonzeros): the split-row path
+  (96 gathered columns + the L2-blocked remainder pass) against a float64 torch.sparse CPU
+  loop over the same A_hat, all ten iterations;
+* config 4 row-partitioned over 2 and 4 ranks sharing the one GPU (gloo exchange, with and
+  without the overlapped local/remote split), each rank against the float64 oracle:
+  tests/dist_worker.py launched by torch.distributed.run as fresh child processes.
+"""
+
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+import torch
+
+from oracle import ppnp_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _workload(name):
+    from ppnp_amd import synth
+
+    n, m, F, K, alpha, dtype = synth.CONFIGS[name]
+    indptr, indices = synth.graph_for(name, device=DEV)
+    H = synth.features(n, F, dtype=dtype, device=DEV)
+    return n, F, K, alpha, dtype, indptr, indices, H
+
+
+def _adj(indptr, indices, n):
+    ix = indices.cpu().numpy()
+    return sp.csr_matrix((np.ones(len(ix), dtype=np.float32), ix, indptr.cpu().numpy()),
+                         shape=(n, n))
+
+
+@pytest.mark.parametrize("name", ["pubmed-synth", "arxiv-synth"])
+def test_config_fp32_full_size_matches_oracle(name):
+    import ppnp_amd
+
+    n, F, K, alpha, dtype, indptr, indices, H = _workload(name)
+    G = ppnp_amd.Graph.from_csr(indptr, indices, None, n, device=DEV, features=F, dtype=dtype)
+    Z = ppnp_amd.propagate_forward(G, H, K, alpha)
+    ref = O.appnp_propagate(O.calc_a_hat(_adj(indptr, indices, n), "sym"),
+                            H.double().cpu().numpy(), K, alpha)
+    err = np.abs(Z.double().cpu().numpy() - ref).max()
+    assert err <= 1e-5 * np.abs(ref).max() + 1e-6, err
+    # the captured plan (hipGraph of the K launches) gives the same bits
+    from ppnp_amd.ops import PropagatePlan
+
+    plan = PropagatePlan(G, H, K, alpha)
+    try:
+        assert torch.equal(plan(), Z)
+    finally:
+        plan.close()
+
+
+def test_config3_msacad_bf16_full_size():
+    import ppnp_amd
+
+    n, F, K, alpha, dtype, indptr, indices, H = _workload("ms-academic-synth")
+    assert dtype == torch.bfloat16 and K == 20
+    G = ppnp_amd.Graph.from_csr(indptr, indices, None, n, device=DEV)
+    Z = ppnp_amd.propagate_forward(G, H, K, alpha)
+    ref = O.appnp_propagate(O.calc_a_hat(_adj(indptr, indices, n), "sym"),
+                            H.float().double().cpu().numpy(), K, alpha)
+    got = Z.float().double().cpu().numpy()
+    assert np.abs(got - ref).max() <= 2e-2 * np.abs(ref).max()
+    assert (got.argmax(1) == ref.argmax(1)).mean() >= 0.98
+
+
+def test_products_k10_matches_oracle():
+    """Config 5 at full size, K = 10, on the split-row path -- every one of the 244.9 M values."""
+    import ppnp_amd
+
+    n, F, K, alpha, dtype, indptr, indices, H = _workload("products-synth")
+    G = ppnp_amd.Graph.from_csr(indptr, indices, None, n, device=DEV, features=F, dtype=dtype)
+    assert G.split_point(F) == 96  # the bench's path: 3 gathered lines + remainder pass
+    Z = ppnp_amd.propagate_forward(G, H, K, alpha).cpu()
+    rp, col, val, _ = G.csr()
+    del indices, G
+    a = torch.sparse_csr_tensor(rp.cpu().long(), col.cpu().long(), val.cpu().double(),
+                                size=(n, n))
+    del rp, col, val
+    torch.set_num_threads(max(1, min(16, len(os.sched_getaffinity(0)))))
+    Hc = H.cpu().double()
+    ref = O.appnp_propagate_torch_cpu(a, Hc, K, alpha)  # float64 operator and iterates
+    err = float((Z.double() - ref).abs().max())
+    tol = 1e-5 * float(ref.abs().max()) + 1e-6
+    assert err <= tol, (err, tol)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("ranks,extra", [(2, []), (2, ["--overlap"]), (4, []),
+                                         (4, ["--overlap"])])
+def test_arxiv_row_partition_matches_oracle(ranks, extra):
+    """Config 4 row-partitioned: each rank's block of Z_K (real HIP kernels, gloo exchange
+    staged through host memory since the ranks share one GPU) against the float64 oracle."""
+    env = dict(os.environ, PPNP_DIST_BACKEND="gloo", PYTHONPATH=ROOT,
+               OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={ranks}", "--master-addr=127.0.0.1",
+           f"--master-port={_free_port()}", os.path.join(ROOT, "tests", "dist_worker.py"),
+           "--layout", "row", "--workload", "arxiv-synth", "--oracle", *extra]
+    proc = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=110)
+    lines = [l for l in proc.stdout.splitlines() if l.startswith("[dist_worker]")]
+    assert proc.returncode == 0, proc.stdout[-3000:] + proc.stderr[-3000:]
+    assert len(lines) == ranks and all(l.endswith("OK") for l in lines), lines
+
+
+def test_stream_done_orders_consumer_after_side_stream():
+    """The hand-off of the relayed exchange (dist.MultipathComm on 'nccl'): work queued on a
+    side stream, then _StreamDone.wait() on the caller's stream -- a consumer queued after the
+    wait sees the side stream's writes even when that work is still running at enqueue time."""
+    from ppnp_amd.dist import _StreamDone
+
+    main = torch.cuda.current_stream()
+    side = torch.cuda.Stream()
+    x = torch.zeros(1 << 20, device=DEV)
+    side.wait_stream(main)
+    with torch.cuda.stream(side):
+        torch.cuda._sleep(20_000_000)  # keep the side stream busy past the enqueue below
+        x.fill_(1.0)
+        ev = torch.cuda.Event()
+        ev.record(side)
+    _StreamDone(ev).wait()
+    y = x * 2.0  # on the main stream
+    assert bool((y == 2.0).all())
+    _StreamDone(None).wait()  # a synchronous exchange hands over no event

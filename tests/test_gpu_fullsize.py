@@ -33,7 +33,7 @@ def graph_sym(products):
     import ppnp_amd
 
     return ppnp_amd.Graph.from_csr(products["indptr"], products["indices"], None, products["n"],
-                                   device=DEV)
+                                   device=DEV, features=products["F"])
 
 
 def _deg(graph):

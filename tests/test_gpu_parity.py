@@ -571,6 +571,92 @@ def test_minibatch_forward_like_batch_main(cora):
     assert np.abs(out - ref).max() <= 1e-4 * np.abs(ref).max()
 
 
+def test_batch_main_loop_runs_unchanged_on_appnp(cora):
+    """batch-main.py:140-146 verbatim against an APPNP model: ``model.ppr[idx_batch]`` is the
+    lazy dense PPR (K chosen to converge), the minibatch logits equal the reference's
+    PPNP.forward fixture, and ``ppr_topk`` reproduces the sparsified buffer of
+    batch-main.py:115-116."""
+    pa = _lib()
+    adj = adj_of(cora)
+    C = int(cora["n_classes"])
+    X = torch.from_numpy(cora["ppnp_X"]).to(DEV)
+    model = pa.APPNP(n_features=X.shape[1], n_classes=C, adj=adj).to(DEV).eval()
+    model.encoder[1].weight.data.copy_(torch.from_numpy(cora["ppnp_W1"]))
+    model.encoder[4].weight.data.copy_(torch.from_numpy(cora["ppnp_W2"]))
+    idx_batch = torch.from_numpy(cora["ppnp_idx"][:32]).to(DEV)
+    # --- batch-main.py:140-146, unchanged ---
+    ppr_sub = model.ppr[idx_batch]
+    sel = (ppr_sub > 0).any(dim=0)
+    ppr_sub = ppr_sub[:, sel]
+    X_batch = X[sel].cuda()
+    with torch.no_grad():
+        logits = model(X_batch, idx=None, ppr=ppr_sub)
+    # ---
+    ref = cora["ppnp_logits"][:32]
+    assert np.abs(logits.cpu().numpy() - ref).max() <= 1e-4 * np.abs(ref).max()
+    full = torch.FloatTensor(O.compute_ppr(adj, alpha=0.1))
+    assert (model.ppr.cpu() - full).abs().max() <= 1e-5 * full.abs().max()
+    model.ppr_topk = 64
+    thresh, _ = full.topk(64, axis=-1)
+    kept, kept_ref = model.ppr.cpu() > 0, full >= thresh[:, -1]
+    assert (kept != kept_ref).float().mean() < 1e-3
+
+
+def test_compiled_training_step_matches_eager(cora):
+    """torch.compile(fullgraph=True) of the main.py:121-127 training step (forward, loss with
+    the L2 term, backward) through the ``ppnp_amd::propagate`` op: no graph break (fullgraph
+    raises on one), and loss and gradients bit-identical to eager.  Dropout off so both runs
+    draw no random numbers."""
+    import torch.nn.functional as Fn
+
+    pa = _lib()
+    C = int(cora["n_classes"])
+    X = torch.from_numpy(cora["ppnp_X"]).to(DEV)
+    n = X.shape[0]
+    idx = torch.from_numpy(cora["ppnp_idx"]).to(DEV)
+    y = torch.randint(0, C, (idx.numel(),), generator=torch.Generator().manual_seed(3)).to(DEV)
+    torch.manual_seed(0)
+    eager = pa.APPNP(n_features=X.shape[1], n_classes=C, adj=adj_of(cora), drop_prob=0.0).to(DEV)
+    comp = pa.APPNP(n_features=X.shape[1], n_classes=C, adj=adj_of(cora), drop_prob=0.0).to(DEV)
+    comp.load_state_dict(eager.state_dict())
+    eager.graph(), comp.graph()  # A_hat built eagerly (setup, not traced)
+
+    def loss_fn(model, X, idx, y):
+        logits = model(X, idx)
+        return Fn.cross_entropy(logits, y) + 5e-3 / 2 * model.get_norm()
+
+    compiled = torch.compile(loss_fn, backend="aot_eager", fullgraph=True)
+    for model, fn in ((eager, loss_fn), (comp, compiled)):
+        model.train()
+        model.zero_grad()
+        fn(model, X, idx, y).backward()
+    le = loss_fn(eager, X, idx, y)
+    lc = compiled(comp, X, idx, y)
+    assert torch.equal(le, lc)
+    for (name, pe), pc in zip(eager.named_parameters(), comp.parameters()):
+        assert torch.equal(pe.grad, pc.grad), name
+    assert n == int(cora["n"])
+
+
+def test_appnp_memo_new_tensor_same_address(cora):
+    """Two fresh X tensors in a row under no_grad: the second may land at the address the
+    first just freed, with the same shape and version 0 -- it must still be propagated
+    (the memo keys on the tensor objects, not on their addresses)."""
+    pa = _lib()
+    n = int(cora["n"])
+    F = int(cora["ppnp_X"].shape[1])
+    ap = pa.APPNP(n_features=F, n_classes=int(cora["n_classes"]), adj=adj_of(cora)).to(DEV)
+    ap.eval()
+    idx = torch.arange(n, device=DEV)
+    outs = []
+    with torch.no_grad():
+        for s in range(3):
+            g = torch.Generator(device=DEV).manual_seed(100 + s)
+            outs.append(ap(torch.randn(n, F, device=DEV, generator=g), idx).clone())
+    assert ap.memo_hits == 0
+    assert not torch.equal(outs[0], outs[1]) and not torch.equal(outs[1], outs[2])
+
+
 # ---------------------------------------------------------------------------------------
 # sparse encoder input (model.py:36-38, 47 on a CSR X): appnp_spmm / appnp_csr_transpose
 # ---------------------------------------------------------------------------------------

@@ -48,7 +48,7 @@ def ahat(adj):
 def graphs(adj):
     import ppnp_amd
 
-    split = ppnp_amd.Graph.from_scipy(adj, device=DEV)  # default: source blocks (n > 65536)
+    split = ppnp_amd.Graph.from_scipy(adj, device=DEV, source_blocks=True)
     plain = ppnp_amd.Graph.from_scipy(adj, device=DEV, source_blocks=False)
     return split, plain
 
@@ -151,7 +151,7 @@ def test_split_point_follows_gather_locality(graphs):
     assert graphs[0].split_point(100, torch.bfloat16) == 0
     assert graphs[1].split_point(100) == 0  # built without source blocks
     ip, ix = synth.community_graph_device(N, 1_500_000, 7, device=DEV)
-    local = ppnp_amd.Graph.from_csr(ip, ix, None, N, device=DEV)
+    local = ppnp_amd.Graph.from_csr(ip, ix, None, N, device=DEV, source_blocks=True)
     assert local.split_point(100) == 0
 
 
@@ -166,7 +166,7 @@ def test_split_weighted_and_rw(adj, mode):
     w.data = rng.uniform(0.5, 2.0, size=w.nnz).astype(np.float32)
     w = ((w + w.T) * 0.5).tocsr()
     w.sort_indices()
-    G = ppnp_amd.Graph.from_scipy(w, mode=mode, device=DEV)
+    G = ppnp_amd.Graph.from_scipy(w, mode=mode, device=DEV, features=100)
     assert G.split_point(100) == 96
     H = _h(100, 14)
     Z = ppnp_amd.propagate_forward(G, H.to(DEV), 3, 0.15, p_drop=0.2, seed=5)

@@ -40,7 +40,7 @@ def main():
                 fh.write(json.dumps(r) + "\n")
     with open(os.path.join(PROF, f"{tag}_dist_check.txt"), "w") as fh:
         for log in sorted(glob.glob(os.path.join(OUT, "dc_*.log"))):
-            lines = [l for l in open(log) if l.startswith("[dist_check]")]
+            lines = [l for l in open(log) if l.startswith(("[dist_check]", "[dist_worker]"))]
             fh.write(f"# {os.path.basename(log)}\n" + "".join(sorted(lines)))
     if os.path.isdir(os.path.join(OUT, "pmc_fetch")):
         subprocess.run([sys.executable, os.path.join(ROOT, "tools", "summarize_profile.py"), tag,

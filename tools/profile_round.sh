@@ -19,12 +19,12 @@ tools/gpu_session.sh \
  "emu_r2c4::200::$B --layout 2x4 --emulate 8:0" \
  "emu_r2c4ov::200::$B --layout 2x4 --overlap --emulate 8:0" \
  "emu_r4c2::200::$B --layout 4x2 --emulate 8:0" \
- "dc_col::200::$TR --nproc-per-node 2 tools/dist_check.py --layout col" \
- "dc_row::300::$G --nproc-per-node 2 tools/dist_check.py --layout row" \
- "dc_row_ov::300::$G --nproc-per-node 2 tools/dist_check.py --layout row --overlap --p-drop 0.3" \
- "dc_2x2::300::$G --nproc-per-node 4 tools/dist_check.py --layout 2x2" \
- "dc_2x4_mp::300::$G --nproc-per-node 8 tools/dist_check.py --layout 2x4 --overlap --p-drop 0.3" \
- "dc_4x2_mp::300::$G --nproc-per-node 8 tools/dist_check.py --layout 4x2" \
+ "dc_col::200::$TR --nproc-per-node 2 tests/dist_worker.py --layout col" \
+ "dc_row::300::$G --nproc-per-node 2 tests/dist_worker.py --layout row" \
+ "dc_row_ov::300::$G --nproc-per-node 2 tests/dist_worker.py --layout row --overlap --p-drop 0.3" \
+ "dc_2x2::300::$G --nproc-per-node 4 tests/dist_worker.py --layout 2x2" \
+ "dc_2x4_mp::300::$G --nproc-per-node 8 tests/dist_worker.py --layout 2x4 --overlap --p-drop 0.3" \
+ "dc_4x2_mp::300::$G --nproc-per-node 8 tests/dist_worker.py --layout 4x2" \
  "w_pubmed::200::$B --workload pubmed-synth" \
  "w_msacad::200::$B --workload ms-academic-synth" \
  "w_arxiv::200::$B --workload arxiv-synth" \
