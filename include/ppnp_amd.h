@@ -59,11 +59,13 @@ enum appnp_norm { APPNP_NORM_SYM = 0, APPNP_NORM_RW = 1 };
  * for 'sym' on an undirected graph, where A_hat^T == A_hat. */
 #define APPNP_GRAPH_TRANSPOSE 0x100
 
-/* OR into `mode`: also keep a copy of A_hat blocked by source rows (2^17 per block; full
- * graphs only).  appnp_propagate then takes the last 1-4 columns of fp32 rows with
- * F = 32q + r (e.g. F = 100) out of the random gather and forms their product in an
- * L2-resident pass, so a gathered row costs q cache lines instead of q + 1.  Costs one more
- * copy of col/val plus (n/2^17 + 1) * n int32 offsets of device memory. */
+/* OR into `mode`: also keep a copy of A_hat regrouped by source block (2^16 source rows per
+ * block; full graphs only).  appnp_propagate then takes the last 1-4 columns of fp32 rows
+ * with F = 32q + r (e.g. F = 100) out of the random gather and forms their product in one
+ * persistent, L2-resident pass per iteration, so a gathered row costs q cache lines instead
+ * of q + 1.  Costs 8 bytes per nonzero plus one int32 per (block, 640-row group) of device
+ * memory.  Best-effort: when the copy cannot be built (too many blocks, device memory), the
+ * graph is still created and gathers whole rows; appnp_graph_source_blocks tells. */
 #define APPNP_GRAPH_SOURCE_BLOCKS 0x200
 
 /* storage type of H / Z (accumulation is always fp32) */
@@ -152,12 +154,16 @@ int appnp_graph_csr(const appnp_graph* g, const int32_t** row_ptr, const int32_t
 int appnp_graph_copy_csr(const appnp_graph* g, int32_t* row_ptr, int32_t* col, float* val,
                          double* dinv, void* stream);
 
+/* Device bytes of the source-blocked copy (APPNP_GRAPH_SOURCE_BLOCKS); 0 if not built. */
+int appnp_graph_source_blocks(const appnp_graph* g, int64_t* bytes);
+
 /* Device view of the fp64 inverse-degree vector (1/sqrt(D) for sym, 1/D for rw), length n. */
 int appnp_graph_dinv(const appnp_graph* g, const double** dinv);
 
 /* Bytes of workspace appnp_propagate / appnp_propagate_bwd need for this shape.  The
  * workspace holds the ping-pong iterates with its own line-aligned leading dimension
- * (`ld` is accepted for ABI stability and ignored). */
+ * (`ld` is accepted for ABI stability and ignored), and, on a graph with source blocks, the
+ * remainder pass's pacing counters (zeroed by each call). */
 size_t appnp_workspace_bytes(const appnp_graph* g, int64_t f, int64_t ld, int dtype);
 
 /* The column split appnp_propagate uses for this shape when H, Z and the workspace are 16-B

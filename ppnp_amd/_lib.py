@@ -50,6 +50,7 @@ _SIGS = {
     "appnp_graph_dinv": (_i32, [_vp, C.POINTER(_vp)]),
     "appnp_workspace_bytes": (_sz, [_vp, _i64, _i64, _i32]),
     "appnp_propagate_split_point": (_i32, [_vp, _i64, _i32, C.POINTER(_i64)]),
+    "appnp_graph_source_blocks": (_i32, [_vp, C.POINTER(_i64)]),
     "appnp_propagate": (
         _i32,
         [_vp, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _f32, _f32, _u64, _vp, _sz, _vp],

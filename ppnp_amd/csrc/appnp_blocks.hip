@@ -1,4 +1,5 @@
-// appnp_blocks.hip -- remainder columns of a row through an L2-resident pass (gfx950).
+// appnp_blocks.hip -- remainder columns of a row through one persistent, L2-resident pass
+// per iteration (gfx950).
 //
 // Why.  The SpMM is bound by random 128-B line requests: every nonzero
 // gathers one row of Z.  An fp32 row of F = 32q + r features (1 <= r <= 4: F = 100 is
@@ -7,17 +8,29 @@
 //
 //   * Z between iterations is kept "split": Z_main [n, 32q] (rows of whole lines, so a
 //     gather is exactly q lines) and Z_rem [n, 4] (16 B per row).
-//   * The remainder product  R = (M_k o A_hat) Z_rem  runs as a pass over A_hat blocked by
-//     SOURCE rows: block b holds the entries whose column lies in [b*2^17, (b+1)*2^17), i.e.
-//     2 MB of Z_rem, which stays resident in every XCD's 4 MB L2 while the block's launch
-//     gathers from it.  One launch per block accumulates into R in block order (fixed order:
-//     bitwise deterministic).
-//   * The main kernel gathers the q lines of Z_main per nonzero and takes R as the
-//     remainder lanes' pre-summed accumulator (appnp_spmm.hip wave_row, StepArgs::rem_in).
+//   * The remainder product  R = (M_k o A_hat) Z_rem  runs as ONE launch per iteration that
+//     sweeps A_hat by SOURCE block: block b holds the entries whose column lies in
+//     [b * 2^16, (b+1) * 2^16), i.e. 1 MB of Z_rem, which sits in every XCD's 4 MB L2 while
+//     the chip gathers from it.  All workgroups walk the blocks in the same order, paced so
+//     that none runs more than one block ahead of the slowest: at most two blocks are live.
 //
-// The blocked copy of A_hat (APPNP_GRAPH_SOURCE_BLOCKS) is built at graph creation:
-// sb_ptr[b * rows + i] is the first entry of row i in block b (block-major, row-minor, so the
-// entries of one block are contiguous and one launch streams them once).
+// The accumulators never leave the chip.  The launch is persistent -- one 1024-thread
+// workgroup per CU, each of its 16 waves owning a group of <= 640 destination rows whose
+// 16-B sums live in that wave's slice of LDS (16 x 640 x 16 B = 160 KiB) across all blocks.
+// (The round-1 form launched once per block and re-read / re-wrote a [n, 4] accumulator in
+// HBM every launch: 19 launches and ~2.7 GB of streams per products-synth iteration.)
+//
+// Work inside a wave is entry-parallel, so hub rows and ragged groups cost no idle lanes:
+// the wave streams its segment of entries (block b, its group) 64 at a time -- one entry per
+// lane, sorted by (row, column) -- gathers Z_rem[column] from L2, and combines the products
+// of equal rows with a segmented inclusive scan over the lanes (DPP row shifts + row
+// broadcasts, fixed order); each segment's last lane adds the sum into its row's LDS slot.
+// The order of every addition is fixed by the layout: bitwise deterministic run to run.
+//
+// The regrouped copy of A_hat (APPNP_GRAPH_SOURCE_BLOCKS) is built at graph creation: entries
+// of segment (pass, block, group) are contiguous, packed as (row in group << 20 | column in
+// block) with their fp32 value; rb_off holds one start per segment -- passes x blocks x
+// (CUs x 16) ints, linear in n (one int per 2^16 x 640 tile of A_hat, ~0.6 MB on products).
 #include <algorithm>
 #include <cstdlib>
 
@@ -27,76 +40,84 @@
 namespace appnp {
 namespace {
 
-// entries of each (block, row): the row's columns are sorted, so a block is a contiguous run.
-// Also counts the off-diagonal entries within kNearRows of their row (*near: gather locality).
-__global__ __launch_bounds__(kBlock) void k_sb_count(const int32_t* __restrict__ rp,
-                                                     const int32_t* __restrict__ col, int64_t rows,
-                                                     int64_t row_lo, int brows,
-                                                     int32_t* __restrict__ cnt,
-                                                     unsigned long long* __restrict__ near) {
-  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  unsigned long long nr = 0;
-  if (i < rows) {
-    int cur = -1, c = 0;
-    for (int32_t e = rp[i]; e < rp[i + 1]; ++e) {
-      const int32_t j = col[e];
-      const int64_t d = (int64_t)j - (row_lo + i);
-      nr += (d != 0 && d < kNearRows && d > -kNearRows) ? 1 : 0;  // the diagonal is no gather
-      const int b = j / brows;
-      if (b != cur) {
-        if (cur >= 0) cnt[(int64_t)cur * rows + i] = c;
-        cur = b;
-        c = 0;
-      }
-      ++c;
-    }
-    if (cur >= 0) cnt[(int64_t)cur * rows + i] = c;
-  }
-#pragma unroll
-  for (int off = 1; off < kWave; off <<= 1) nr += __shfl_xor(nr, off);
-  if ((threadIdx.x & (kWave - 1)) == 0 && nr) atomicAdd(near, nr);
-}
+constexpr int kRemThreads = kRemWaves * kWave;  // 1024
+constexpr int kRemLdsBytes = 160 * 1024;        // LDS per CU on gfx950
+constexpr int kRemMaxRg = kRemLdsBytes / (kRemWaves * 16);  // 640 rows per wave group
+constexpr uint32_t kRemNone = 0xffffffffu;      // packed entry of an idle lane (row 4095)
+constexpr int kWalkWaves = kWavesPerBlock;      // build walk: one wave per group
+constexpr int kWalkMaxBlocks = 4096;            // LDS cursors of the build walk: 64 KiB
+constexpr int kPaceSpins = 2048;                // bounded pacing wait (then run free)
 
-__global__ __launch_bounds__(kBlock) void k_sb_fill(const int32_t* __restrict__ rp,
-                                                    const int32_t* __restrict__ col,
-                                                    const float* __restrict__ val, int64_t rows,
-                                                    int brows, const int32_t* __restrict__ ptr,
-                                                    int32_t* __restrict__ bcol,
-                                                    float* __restrict__ bval) {
-  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (i >= rows) return;
-  int cur = -1;
-  int32_t pos = 0;
-  for (int32_t e = rp[i]; e < rp[i + 1]; ++e) {
-    const int32_t c = col[e];
-    const int b = c / brows;
-    if (b != cur) {
-      cur = b;
-      pos = ptr[(int64_t)b * rows + i];
-    }
-    bcol[pos] = c;
-    bval[pos] = val[e];
-    ++pos;
+static_assert(kRemMaxRg < (1 << kRemRowBits), "row in group must fit the packed entry");
+static_assert(kRemRowBits + kRemColBits == 32, "packed entry is 32 bits");
+
+struct RemLayout {
+  const int32_t* off;   // segment starts
+  const uint32_t* ent;  // packed (row in group, column in block)
+  const float* val;
+  int32_t* done;        // [passes * nb] blocks finished, cumulative over the call's iterations
+  int32_t nb, br_log2, slots, rg, passes;
+  int32_t iter;         // index of this launch within the call (pacing target)
+  int32_t pace;         // 0: no pacing
+};
+
+// ---- segmented inclusive scan over the 64 lanes (rows non-decreasing across lanes) --------
+// DPP (gfx9 family): row_shr:n shifts within each 16-lane row; row_bcast:15 / row_bcast:31
+// feed lane 15 of a row / lane 31 to the rows above.  A lane adds the moved partial only when
+// it comes from a lane of the same row index (segment); rows are sorted, so equality of the
+// two end points means every lane between belongs to the segment too.
+constexpr int kDppRowShr1 = 0x111, kDppRowShr2 = 0x112, kDppRowShr4 = 0x114,
+              kDppRowShr8 = 0x118, kDppRowBcast15 = 0x142, kDppRowBcast31 = 0x143;
+
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ void seg_step(int row, f32x4& v) {
+  const int src_row = __builtin_amdgcn_update_dpp(-1, row, CTRL, ROW_MASK, 0xf, false);
+  const float ux = __int_as_float(
+      __builtin_amdgcn_update_dpp(0, __float_as_int(v.x), CTRL, ROW_MASK, 0xf, false));
+  const float uy = __int_as_float(
+      __builtin_amdgcn_update_dpp(0, __float_as_int(v.y), CTRL, ROW_MASK, 0xf, false));
+  const float uz = __int_as_float(
+      __builtin_amdgcn_update_dpp(0, __float_as_int(v.z), CTRL, ROW_MASK, 0xf, false));
+  const float uw = __int_as_float(
+      __builtin_amdgcn_update_dpp(0, __float_as_int(v.w), CTRL, ROW_MASK, 0xf, false));
+  if (src_row == row) {
+    v.x += ux;
+    v.y += uy;
+    v.z += uz;
+    v.w += uw;
   }
 }
 
-// R[i] (+)= sum over the entries of row i in source block b of w_ij * Z_rem[j]; thread per
-// row (a block holds ~nnz/(rows * n_sb) entries of a row: 2.7 on products-synth), U entries
-// loaded and gathered at a time so that a wave's longest row takes few dependent rounds.
-// One launch per block, so all resident waves gather from the same 2 MB of Z_rem; per row the
-// sum runs over blocks in order and entries in column order (fixed: bitwise deterministic).
-// a.zin = Z_rem (n x 4 fp32), a.aux = R (rows x 4 fp32 accumulator).  FIRST: R starts at 0.
-// LAST: the iteration's epilogue, out[i, :nv] = (1-alpha) R[i] + alpha H_rem[i] (a.h = H_rem,
-// a.out / a.ld_out, a.f = nv valid columns: 4 into the next Z_rem, 1-4 into Z's last columns).
-// (A single launch keeping every row's sum in registers while all threads walk the blocks
-// measured slower: threads drift apart and the blocks they gather from no longer fit L2.)
-template <int EPI, bool FIRST, bool LAST>
+__device__ __forceinline__ void seg_scan(int row, f32x4& v) {
+  seg_step<kDppRowShr1, 0xf>(row, v);
+  seg_step<kDppRowShr2, 0xf>(row, v);
+  seg_step<kDppRowShr4, 0xf>(row, v);
+  seg_step<kDppRowShr8, 0xf>(row, v);
+  seg_step<kDppRowBcast15, 0xa>(row, v);  // rows 1, 3 <- lanes 15, 47
+  seg_step<kDppRowBcast31, 0xc>(row, v);  // rows 2, 3 <- lane 31
+}
+
+// Wait (one lane) until every workgroup has finished block b - 2 of this iteration, so the
+// chip gathers from at most two blocks at once.  Bounded: on a timeout the caller stops
+// pacing for the rest of the launch (the result never depends on the pacing, only the L2 hit
+// rate does; a grid larger than the resident set can therefore not deadlock).
+__device__ __forceinline__ bool pace_wait(int32_t* ctr, int target) {
+  __attribute__((address_space(1))) int32_t* c =
+      (__attribute__((address_space(1))) int32_t*)ctr;
+  for (int spin = 0; spin < kPaceSpins; ++spin) {
+    if (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return true;
+    __builtin_amdgcn_s_sleep(4);
+  }
+  return false;
+}
+
+// Epilogue of one row of the iteration: FWD out[i, :nv] = (1-alpha) R[i] + alpha H_rem[i]
+// (a.h = H_rem, a.out / a.ld_out, a.f = nv valid columns: 4 into the next Z_rem, 1-4 into Z's
+// last columns); BWD G_k = (1-alpha) R into the next remainder buffer (none at k = 0) and
+// dH[:, fs:f] += alpha' G_k (a.rem_dh / a.ld_rem_dh).
+template <int EPI>
 __device__ __forceinline__ void rem_finish(const StepArgs& a, int64_t i, f32x4 acc) {
-  if constexpr (!LAST) {
-    static_cast<f32x4*>(a.aux)[i] = acc;
-  } else if constexpr (EPI == EPI_BWD) {
-    // adjoint: G_k = (1-alpha) R into the next remainder buffer (none at k = 0), and
-    // dH[:, fs:f] += alpha' G_k (exactly nv columns)
+  if constexpr (EPI == EPI_BWD) {
     const float y[4] = {a.scale * acc.x, a.scale * acc.y, a.scale * acc.z, a.scale * acc.w};
     if (a.out)
       static_cast<f32x4*>(a.out)[i] = f32x4{y[0], y[1], y[2], y[3]};
@@ -136,82 +157,133 @@ __device__ __forceinline__ void rem_finish(const StepArgs& a, int64_t i, f32x4 a
   }
 }
 
-// Blocks [0, light_blocks): thread per row.  Trailing blocks: hub rows (> kHubRow entries in
-// all, listed in a.hub; the light threads skip them), a wavefront each -- its lanes stride
-// over the row's entries of the block and a fixed butterfly adds them -- so a power-law hub
-// does not serialise one thread while the launch waits.
-template <int U, int EPI, bool FIRST, bool LAST>
-__global__ __launch_bounds__(kBlock) void k_rem_block(StepArgs a, const int32_t* __restrict__ ptr,
-                                                      const int32_t* __restrict__ bcol,
-                                                      const float* __restrict__ bval) {
+// One iteration of the remainder columns over all source blocks (see the file comment).
+// a.zin = Z_rem (n x 4 fp32); U chunks of 64 entries in flight per wave.
+template <int EPI, int U>
+__global__ __launch_bounds__(kRemThreads) void k_rem_persist(StepArgs a, RemLayout L) {
+  extern __shared__ f32x4 rem_acc[];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  f32x4* acc = rem_acc + (int64_t)wv * L.rg;
   const f32x4* __restrict__ z = static_cast<const f32x4*>(a.zin);
-  const f32x4* __restrict__ r = static_cast<const f32x4*>(a.aux);
-  if ((int64_t)blockIdx.x >= a.light_blocks) {
-    const int lane = threadIdx.x & (kWave - 1);
-    const int64_t nw = ((int64_t)gridDim.x - a.light_blocks) * kWavesPerBlock;
-    for (int64_t hw = ((int64_t)blockIdx.x - a.light_blocks) * kWavesPerBlock +
-                      (threadIdx.x >> 6);
-         hw < a.n_hub; hw += nw) {
-      const int64_t i = a.hub[hw];
-      f32x4 acc = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-      const int32_t end = ptr[i + 1];
-      for (int32_t e = ptr[i] + lane; e < end; e += kWave) {
-        const int32_t c = ld_nt<int32_t>(bcol + e);
-        const float w = edge_weight(ld_nt<float>(bval + e), a.row_lo + i, c, a);
-        const f32x4 v = z[c];
-        acc.x = fmaf(w, v.x, acc.x);
-        acc.y = fmaf(w, v.y, acc.y);
-        acc.z = fmaf(w, v.z, acc.z);
-        acc.w = fmaf(w, v.w, acc.w);
-      }
+  const int64_t slot = (int64_t)blockIdx.x * kRemWaves + wv;
+  const uint32_t cmask = (1u << kRemColBits) - 1u;
+  const int target = (L.iter + 1) * (int)gridDim.x;
+  bool pacing = L.pace != 0;
+  for (int p = 0; p < L.passes; ++p) {
+    const int64_t r0 = ((int64_t)p * L.slots + slot) * L.rg;
+    const int rows = (int)max<int64_t>(0, min<int64_t>(L.rg, a.n_rows - r0));
+    for (int r = lane; r < rows; r += kWave) acc[r] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    int32_t* done = L.done + (int64_t)p * L.nb;
+    for (int b = 0; b < L.nb; ++b) {
+      if (b >= 2 && threadIdx.x == 0 && pacing) pacing = pace_wait(done + b - 2, target);
+      __syncthreads();
+      const int64_t sg = ((int64_t)p * L.nb + b) * L.slots + slot;
+      const int32_t beg = L.off[sg], end = L.off[sg + 1];
+      const int64_t cbase = (int64_t)b << L.br_log2;
+      for (int32_t c0 = beg; c0 < end; c0 += kWave * U) {
+        uint32_t en[U];
+        float wt[U];
+        f32x4 zv[U];
 #pragma unroll
-      for (int off = 1; off < kWave; off <<= 1) {
-        acc.x += __shfl_xor(acc.x, off);
-        acc.y += __shfl_xor(acc.y, off);
-        acc.z += __shfl_xor(acc.z, off);
-        acc.w += __shfl_xor(acc.w, off);
-      }
-      if (lane == 0) {
-        if constexpr (!FIRST) {
-          const f32x4 p = r[i];
-          acc = f32x4{p.x + acc.x, p.y + acc.y, p.z + acc.z, p.w + acc.w};
+        for (int u = 0; u < U; ++u) {
+          const int32_t e = c0 + u * kWave + lane;
+          en[u] = kRemNone;
+          wt[u] = 0.0f;
+          if (e < end) {
+            en[u] = ld_nt<uint32_t>(L.ent + e);
+            wt[u] = ld_nt<float>(L.val + e);
+          }
         }
-        rem_finish<EPI, FIRST, LAST>(a, i, acc);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          zv[u] = en[u] != kRemNone ? z[cbase + (en[u] & cmask)] : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (c0 + u * kWave >= end) break;  // wave-uniform
+          const bool act = en[u] != kRemNone;
+          const int row = (int)(en[u] >> kRemColBits);
+          const float w =
+              act ? edge_weight(wt[u], r0 + row, (int32_t)(cbase + (en[u] & cmask)), a) : 0.0f;
+          f32x4 v = f32x4{w * zv[u].x, w * zv[u].y, w * zv[u].z, w * zv[u].w};
+          seg_scan(row, v);
+          const int prev = __shfl_up(row, 1);
+          const unsigned long long heads = __ballot(lane == 0 || prev != row);
+          const bool tail = lane == kWave - 1 || ((heads >> (lane + 1)) & 1ull);
+          if (act && tail) {
+            const f32x4 c = acc[row];
+            acc[row] = f32x4{c.x + v.x, c.y + v.y, c.z + v.z, c.w + v.w};
+          }
+        }
       }
+      __syncthreads();
+      if (threadIdx.x == 0 && L.pace)
+        __hip_atomic_fetch_add((__attribute__((address_space(1))) int32_t*)(done + b), 1,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    return;
+    for (int r = lane; r < rows; r += kWave) rem_finish<EPI>(a, r0 + r, acc[r]);
   }
-  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (i >= a.n_rows) return;
-  if (a.n_hub && a.row_ptr[i + 1] - a.row_ptr[i] > kHubRow) return;  // hub: trailing blocks
-  f32x4 acc = FIRST ? f32x4{0.0f, 0.0f, 0.0f, 0.0f} : r[i];
-  const int32_t end = ptr[i + 1];
-  for (int32_t e = ptr[i]; e < end; e += U) {
-    int32_t c[U];
-    float w[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      c[u] = 0;
-      w[u] = 0.0f;
-      if (e + u < end) {  // cached: neighbouring lanes' runs share lines (non-temporal: -1 %)
-        c[u] = bcol[e + u];
-        w[u] = bval[e + u];
+}
+
+// Build walk: one wave per group, walking the group's rows in order with one cursor per
+// source block in LDS.  COUNT: the number of entries of each (pass, block, group) segment
+// into cnt, plus the off-diagonal entries within kNearRows of their row (gather locality).
+// FILL: cursors start at the segment offsets; every entry is written to its slot.  A row's
+// columns are sorted, so its entries of one block are a run of consecutive lanes.
+template <bool FILL>
+__global__ __launch_bounds__(kBlock) void k_rb_walk(const int32_t* __restrict__ rp,
+                                                    const int32_t* __restrict__ col,
+                                                    const float* __restrict__ val, int64_t n,
+                                                    int rg, int slots, int nb, int br_log2,
+                                                    int64_t n_groups, int32_t* __restrict__ cnt,
+                                                    const int32_t* __restrict__ off,
+                                                    uint32_t* __restrict__ ent,
+                                                    float* __restrict__ bval,
+                                                    unsigned long long* __restrict__ near) {
+  extern __shared__ int32_t walk_cur[];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int w = threadIdx.x >> 6;
+  int32_t* cur = walk_cur + (int64_t)w * nb;
+  const int64_t g = (int64_t)blockIdx.x * kWalkWaves + w;
+  if (g >= n_groups) return;  // no workgroup barrier in this kernel
+  const int64_t p = g / slots, s = g - p * slots;
+  for (int b = lane; b < nb; b += kWave) cur[b] = FILL ? off[(p * nb + b) * slots + s] : 0;
+  const int64_t r0 = g * rg, r1 = min<int64_t>(n, r0 + rg);
+  unsigned long long nr = 0;
+  for (int64_t i = r0; i < r1; ++i) {
+    const int32_t beg = rp[i], end = rp[i + 1];
+    for (int32_t e0 = beg; e0 < end; e0 += kWave) {
+      const int32_t e = e0 + lane;
+      const bool act = e < end;
+      const int32_t c = act ? col[e] : 0;
+      const int b = act ? (c >> br_log2) : INT32_MAX;
+      const int bprev = __shfl_up(b, 1);
+      const unsigned long long heads = __ballot(act && (lane == 0 || bprev != b));
+      const unsigned long long upto = lane == kWave - 1 ? ~0ull : ((2ull << lane) - 1ull);
+      const int head = 63 - __clzll(heads & upto);  // first lane of this lane's run
+      const int bnext = __shfl_down(b, 1);
+      const bool tail = act && (lane == kWave - 1 || bnext != b);
+      int32_t base = 0;
+      if (act) base = cur[b];
+      if constexpr (FILL) {
+        if (act) {
+          const int32_t pos = base + (lane - head);
+          ent[pos] = ((uint32_t)(i - r0) << kRemColBits) | ((uint32_t)c & ((1u << kRemColBits) - 1u));
+          bval[pos] = val[e];
+        }
+      } else {
+        const int64_t d = (int64_t)c - i;
+        nr += (act && d != 0 && d < kNearRows && d > -kNearRows) ? 1 : 0;
       }
-    }
-    f32x4 v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      v[u] = e + u < end ? z[c[u]] : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const float wu = e + u < end ? edge_weight(w[u], a.row_lo + i, c[u], a) : 0.0f;
-      acc.x = fmaf(wu, v[u].x, acc.x);
-      acc.y = fmaf(wu, v[u].y, acc.y);
-      acc.z = fmaf(wu, v[u].z, acc.z);
-      acc.w = fmaf(wu, v[u].w, acc.w);
+      if (tail) cur[b] = base + (lane - head + 1);
     }
   }
-  rem_finish<EPI, FIRST, LAST>(a, i, acc);
+  if constexpr (!FILL) {
+    for (int b = lane; b < nb; b += kWave) cnt[(p * nb + b) * slots + s] = cur[b];
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) nr += __shfl_xor(nr, o);
+    if (lane == 0 && nr) atomicAdd(near, nr);
+  }
 }
 
 // H [n, ld_h] -> the split layout: main [n, fs] (whole lines per row) and rem [n, 4]
@@ -249,44 +321,77 @@ __global__ __launch_bounds__(kBlock) void k_split_copy(const float* __restrict__
   }
 }
 
+template <int EPI>
+hipError_t launch_rem(dim3 grid, dim3 block, size_t lds, hipStream_t s, const StepArgs& a,
+                      const RemLayout& L) {
+  constexpr int kU = 2;  // chunks of 64 entries in flight per wave
+  static const hipError_t attr = hipFuncSetAttribute(  // > 64 KiB of dynamic LDS, once
+      reinterpret_cast<const void*>(k_rem_persist<EPI, kU>),
+      hipFuncAttributeMaxDynamicSharedMemorySize, kRemLdsBytes);
+  if (attr != hipSuccess) return attr;
+  hipLaunchKernelGGL((k_rem_persist<EPI, kU>), grid, block, lds, s, a, L);
+  return hipGetLastError();
+}
+
+int env_or(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return (v && *v) ? atoi(v) : dflt;
+}
+
 }  // namespace
 
+// The regrouped copy of A_hat for the persistent remainder pass.  Best-effort at the caller
+// (appnp_graph_create_rows): APPNP_ENOTSUP / APPNP_ERANGE / APPNP_ENOMEM leave the graph
+// without it, and appnp_propagate gathers whole rows.
 int graph_build_source_blocks(appnp_graph* g, hipStream_t s) {
   const int64_t rows = g->row_hi - g->row_lo;
-  static const int brows = [] {
-    const char* v = getenv("APPNP_SB_ROWS");  // measurement override of kSourceBlockRows
-    const int x = (v && *v) ? atoi(v) : kSourceBlockRows;
-    return x >= 1024 ? x : kSourceBlockRows;
+  if (g->row_lo != 0 || rows != g->n) return APPNP_EINVAL;
+  // APPNP_SB_ROWS: measurement override of the block size (a power of two, 2^10..2^20 rows)
+  static const int br_log2 = [] {
+    const int x = env_or("APPNP_SB_ROWS", 1 << kSourceBlockLog2);
+    int l = 10;
+    while (l < kRemColBits && (1 << l) < x) ++l;
+    return l;
   }();
-  const int64_t nb = std::max<int64_t>(1, (g->n + brows - 1) / brows);
-  const int64_t cells = nb * rows;
+  const int64_t nb = std::max<int64_t>(1, (g->n + (1LL << br_log2) - 1) >> br_log2);
+  if (nb > kWalkMaxBlocks) return APPNP_ENOTSUP;
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      cus <= 0)
+    return APPNP_EDEVICE;
+  const int64_t slots = (int64_t)cus * kRemWaves;
+  const int64_t passes = std::max<int64_t>(1, (rows + slots * kRemMaxRg - 1) / (slots * kRemMaxRg));
+  const int64_t rg = std::max<int64_t>(1, (rows + passes * slots - 1) / (passes * slots));
+  const int64_t cells = passes * nb * slots;
   if (cells + 1 > INT32_MAX) return APPNP_ERANGE;
   int rc = APPNP_OK;
   int32_t* cnt = nullptr;
   int64_t *bsum = nullptr, *tot = nullptr;
-  const unsigned grid = (unsigned)std::max<int64_t>(1, (rows + kBlock - 1) / kBlock);
   auto ok = [&](hipError_t e) {
     if (e != hipSuccess && rc == APPNP_OK)
       rc = (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) ? APPNP_ENOMEM
                                                                        : APPNP_EDEVICE;
     return rc == APPNP_OK;
   };
-  if (ok(hipMalloc(&g->sb_ptr, (cells + 1) * sizeof(int32_t))) &&
-      ok(hipMalloc(&g->sb_col, std::max<int64_t>(1, g->nnz_hat) * sizeof(int32_t))) &&
-      ok(hipMalloc(&g->sb_val, std::max<int64_t>(1, g->nnz_hat) * sizeof(float))) &&
-      ok(hipMalloc(&cnt, std::max<int64_t>(1, cells) * sizeof(int32_t))) &&
+  const int64_t n_groups = passes * slots;
+  const unsigned grid = (unsigned)((n_groups + kWalkWaves - 1) / kWalkWaves);
+  const size_t lds = (size_t)kWalkWaves * nb * sizeof(int32_t);
+  const int64_t nnz = std::max<int64_t>(1, g->nnz_hat);
+  if (ok(hipMalloc(&g->rb_off, (cells + 1) * sizeof(int32_t))) &&
+      ok(hipMalloc(&g->rb_ent, nnz * sizeof(uint32_t))) &&
+      ok(hipMalloc(&g->rb_val, nnz * sizeof(float))) &&
+      ok(hipMalloc(&cnt, cells * sizeof(int32_t))) &&
       ok(hipMalloc(&bsum, scan_partials(cells) * sizeof(int64_t))) &&
       ok(hipMalloc(&tot, 2 * sizeof(int64_t))) &&
-      ok(hipMemsetAsync(tot, 0, 2 * sizeof(int64_t), s)) &&
-      ok(hipMemsetAsync(cnt, 0, std::max<int64_t>(1, cells) * sizeof(int32_t), s))) {
-    if (rows > 0) {
-      hipLaunchKernelGGL(k_sb_count, dim3(grid), dim3(kBlock), 0, s, g->row_ptr, g->col, rows,
-                         g->row_lo, brows, cnt, reinterpret_cast<unsigned long long*>(tot + 1));
-      ok(hipGetLastError());
-    }
-    if (rc == APPNP_OK && ok(exclusive_scan(cnt, cells, g->sb_ptr, bsum, tot, s)) && rows > 0) {
-      hipLaunchKernelGGL(k_sb_fill, dim3(grid), dim3(kBlock), 0, s, g->row_ptr, g->col, g->val,
-                         rows, brows, g->sb_ptr, g->sb_col, g->sb_val);
+      ok(hipMemsetAsync(tot, 0, 2 * sizeof(int64_t), s))) {
+    hipLaunchKernelGGL(k_rb_walk<false>, dim3(grid), dim3(kBlock), lds, s, g->row_ptr, g->col,
+                       g->val, rows, (int)rg, (int)slots, (int)nb, br_log2, n_groups, cnt,
+                       nullptr, nullptr, nullptr, reinterpret_cast<unsigned long long*>(tot + 1));
+    if (ok(hipGetLastError()) && ok(exclusive_scan(cnt, cells, g->rb_off, bsum, tot, s))) {
+      hipLaunchKernelGGL(k_rb_walk<true>, dim3(grid), dim3(kBlock), lds, s, g->row_ptr, g->col,
+                         g->val, rows, (int)rg, (int)slots, (int)nb, br_log2, n_groups, nullptr,
+                         g->rb_off, g->rb_ent, g->rb_val, nullptr);
       ok(hipGetLastError());
     }
     int64_t near = 0;
@@ -299,32 +404,42 @@ int graph_build_source_blocks(appnp_graph* g, hipStream_t s) {
   if (bsum) (void)hipFree(bsum);
   if (tot) (void)hipFree(tot);
   if (rc != APPNP_OK) {
-    if (g->sb_ptr) (void)hipFree(g->sb_ptr);
-    if (g->sb_col) (void)hipFree(g->sb_col);
-    if (g->sb_val) (void)hipFree(g->sb_val);
-    g->sb_ptr = g->sb_col = nullptr;
-    g->sb_val = nullptr;
+    if (g->rb_off) (void)hipFree(g->rb_off);
+    if (g->rb_ent) (void)hipFree(g->rb_ent);
+    if (g->rb_val) (void)hipFree(g->rb_val);
+    g->rb_off = nullptr;
+    g->rb_ent = nullptr;
+    g->rb_val = nullptr;
     return rc;
   }
-  g->n_sb = (int32_t)nb;
+  g->rb_nb = (int32_t)nb;
+  g->rb_br_log2 = br_log2;
+  g->rb_grid = cus;
+  g->rb_slots = (int32_t)slots;
+  g->rb_rg = (int32_t)rg;
+  g->rb_passes = (int32_t)passes;
   return APPNP_OK;
 }
 
-// One iteration of the remainder columns: R = (M_k o A_hat) Z_rem over all source blocks, one
-// launch per block in block order, the last one applying the epilogue (k_rem_block).
-// a: the iteration's StepArgs (dropout key, row_lo, n_rows, scale, alpha); z_rem [n, 4];
-// acc [rows, 4] scratch (may be `out` itself when out is a Z_rem buffer); h_rem = H + fs;
-// out / ld_out / nv: where the nv valid columns of Z_{k+1} go.  epi = EPI_BWD (adjoint): h_rem
-// / ld_h are dH's remainder columns, accumulated into; out (G_k's remainder) may be null.
-// Entries in flight per thread: 16 (products-synth per iteration: 1 -> 1.6 ms, 8 -> 1.4 ms,
-// 16 0.05 ms less; tools/sweep_split.sh).  Blocks of 2^17 source rows measured best
-// (2^16, 96k, 160k, 192k and 2^18 rows: +0.01-0.3 ms).
+// Pacing counters of one call (passes x blocks int32), zeroed by the caller once per call.
+size_t remainder_counter_bytes(const appnp_graph* g) {
+  if (!g->rb_off) return 0;
+  return ((size_t)g->rb_passes * g->rb_nb * sizeof(int32_t) + 255) / 256 * 256;
+}
+
+// One iteration of the remainder columns: R = (M_k o A_hat) Z_rem over all source blocks in
+// one persistent launch (k_rem_persist), epilogue included.  a: the iteration's StepArgs
+// (dropout key, n_rows, scale, alpha); z_rem [n, 4]; h_rem = H + fs; out / ld_out / nv: where
+// the nv valid columns of Z_{k+1} go.  epi = EPI_BWD (adjoint): h_rem / ld_h are dH's
+// remainder columns, accumulated into; out (G_k's remainder) may be null.  done: the call's
+// pacing counters (remainder_counter_bytes, zeroed before the first iteration); iter: the
+// launch's index within the call.
 hipError_t launch_remainder(const appnp_graph* g, const StepArgs& a_in, int epi,
-                            const float* z_rem, float* acc, const float* h_rem, int64_t ld_h,
-                            float* out, int64_t ld_out, int nv, hipStream_t s) {
+                            const float* z_rem, const float* h_rem, int64_t ld_h, float* out,
+                            int64_t ld_out, int nv, int32_t* done, int iter, hipStream_t s) {
   StepArgs a = a_in;
   a.zin = z_rem;
-  a.aux = acc;
+  a.aux = nullptr;
   if (epi == EPI_BWD) {  // h_rem / ld_h: dH's remainder columns, accumulated into
     a.h = nullptr;
     a.rem_dh = const_cast<float*>(h_rem);
@@ -336,34 +451,15 @@ hipError_t launch_remainder(const appnp_graph* g, const StepArgs& a_in, int epi,
   a.out = out;
   a.ld_out = ld_out;
   a.f = nv;
-  const int64_t rows = a.n_rows;
-  if (rows <= 0) return hipSuccess;
-  a.row_ptr = g->row_ptr;  // whole-row lengths: hub rows are left to the trailing blocks
-  a.hub = g->hub;
-  a.n_hub = g->hub ? g->n_hub : 0;
-  a.light_blocks = (rows + kBlock - 1) / kBlock;
-  const int64_t heavy = std::min<int64_t>((a.n_hub + kWavesPerBlock - 1) / kWavesPerBlock, 4096);
-  const dim3 grid((unsigned)(a.light_blocks + heavy)), block(kBlock);
-  const int nb = g->n_sb;
-  for (int32_t b = 0; b < nb; ++b) {
-    const int32_t* p = g->sb_ptr + (int64_t)b * rows;
-    const bool first = b == 0, last = b == nb - 1;
-    auto go = [&](auto kern) {
-      hipLaunchKernelGGL(kern, grid, block, 0, s, a, p, g->sb_col, g->sb_val);
-    };
-    if (epi == EPI_BWD) {
-      if (first && last) go(k_rem_block<16, EPI_BWD, true, true>);
-      else if (first) go(k_rem_block<16, EPI_BWD, true, false>);
-      else if (last) go(k_rem_block<16, EPI_BWD, false, true>);
-      else go(k_rem_block<16, EPI_BWD, false, false>);
-    } else {
-      if (first && last) go(k_rem_block<16, EPI_FWD, true, true>);
-      else if (first) go(k_rem_block<16, EPI_FWD, true, false>);
-      else if (last) go(k_rem_block<16, EPI_FWD, false, true>);
-      else go(k_rem_block<16, EPI_FWD, false, false>);
-    }
-  }
-  return hipGetLastError();
+  if (a.n_rows <= 0) return hipSuccess;
+  // APPNP_REM_PACE=0 (measurement): no pacing between the workgroups
+  static const int pace = env_or("APPNP_REM_PACE", 1);
+  RemLayout L{g->rb_off, g->rb_ent, g->rb_val, done, g->rb_nb, g->rb_br_log2, g->rb_slots,
+              g->rb_rg, g->rb_passes, iter, pace && done ? 1 : 0};
+  const size_t lds = (size_t)kRemWaves * g->rb_rg * sizeof(f32x4);
+  const dim3 grid((unsigned)g->rb_grid), block(kRemThreads);
+  if (epi == EPI_BWD) return launch_rem<EPI_BWD>(grid, block, lds, s, a, L);
+  return launch_rem<EPI_FWD>(grid, block, lds, s, a, L);
 }
 
 hipError_t launch_split_copy(const float* h, int64_t ld_h, int64_t n, int64_t f, int64_t fs,

@@ -56,8 +56,11 @@ struct StepArgs {
 constexpr int kHeavyRow = 32;   // a row longer than this gets a whole wavefront (narrow)
 constexpr int kHubRow = 512;    // ... and one longer than this is dispatched first (wide)
 constexpr int kWideAvgRow = 24; // mean row length from which large graphs take a wave per row
-constexpr int kSourceBlockRows = 1 << 17;  // source rows per block of the remainder pass
-                                           // (2 MB of 16-B remainders: L2-resident)
+constexpr int kSourceBlockLog2 = 16;  // source rows per block of the remainder pass: 2^16
+                                     // (1 MB of 16-B remainders; two blocks stay in L2)
+constexpr int kRemWaves = 16;        // waves per workgroup of the persistent remainder pass
+constexpr int kRemColBits = 20;      // column-in-block bits of a packed remainder entry
+constexpr int kRemRowBits = 12;      // row-in-group bits (the rest of the 32)
 constexpr int kNearRows = 1 << 14;  // "near" entry: |col - row| below this (gather locality)
 
 __host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {

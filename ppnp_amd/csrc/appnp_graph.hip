@@ -312,7 +312,7 @@ void graph_free(appnp_graph* g) {
   if (!g) return;
   void* ptrs[] = {g->row_ptr, g->col, g->val, g->lrow_ptr, g->lcol, g->lval,
                   g->rrow_ptr, g->rcol, g->rval, g->dinv, g->t_row_ptr, g->t_col, g->t_val,
-                  g->heavy, g->t_heavy, g->hub, g->t_hub, g->sb_ptr, g->sb_col, g->sb_val};
+                  g->heavy, g->t_heavy, g->hub, g->t_hub, g->rb_off, g->rb_ent, g->rb_val};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   g->row_ptr = g->col = g->lrow_ptr = g->lcol = g->rrow_ptr = g->rcol = nullptr;
@@ -321,9 +321,10 @@ void graph_free(appnp_graph* g) {
   g->t_row_ptr = g->t_col = nullptr;
   g->t_val = nullptr;
   g->heavy = g->t_heavy = g->hub = g->t_hub = nullptr;
-  g->sb_ptr = g->sb_col = nullptr;
-  g->sb_val = nullptr;
-  g->n_sb = 0;
+  g->rb_off = nullptr;
+  g->rb_ent = nullptr;
+  g->rb_val = nullptr;
+  g->rb_nb = g->rb_passes = 0;
 }
 
 #define APPNP_TRY(expr)                                                         \

@@ -37,10 +37,18 @@ struct appnp_graph {
   int32_t* t_row_ptr = nullptr; // A_hat^T (APPNP_GRAPH_TRANSPOSE, when A_hat is not symmetric)
   int32_t* t_col = nullptr;
   float* t_val = nullptr;
-  int32_t* sb_ptr = nullptr;    // A_hat blocked by source rows (APPNP_GRAPH_SOURCE_BLOCKS):
-  int32_t* sb_col = nullptr;    //   [n_sb * rows + 1], block-major (appnp_blocks.hip)
-  float* sb_val = nullptr;
-  int32_t n_sb = 0;
+  // A_hat regrouped for the persistent remainder pass (APPNP_GRAPH_SOURCE_BLOCKS,
+  // appnp_blocks.hip): segment (pass, source block, group) holds the entries of one wave's
+  // group of rows whose column lies in that block, sorted by (row, column)
+  int32_t* rb_off = nullptr;    // [rb_passes * rb_nb * rb_slots + 1] segment starts
+  uint32_t* rb_ent = nullptr;   // [nnz_hat] (row in group << kRemColBits) | column in block
+  float* rb_val = nullptr;      // [nnz_hat]
+  int32_t rb_nb = 0;            // source blocks of 2^rb_br_log2 rows
+  int32_t rb_br_log2 = 0;
+  int32_t rb_grid = 0;          // workgroups of the pass (one per CU)
+  int32_t rb_slots = 0;         // groups per pass = rb_grid * kRemWaves
+  int32_t rb_rg = 0;            // rows per group
+  int32_t rb_passes = 0;
   double near_frac = 0.0;       // off-diagonal entries within kNearRows of their row / nnz
 };
 
@@ -67,9 +75,10 @@ hipError_t exclusive_scan(const int32_t* cnt, int64_t rows, int32_t* out, int64_
 
 // appnp_blocks.hip
 int graph_build_source_blocks(appnp_graph* g, hipStream_t s);
+size_t remainder_counter_bytes(const appnp_graph* g);
 hipError_t launch_remainder(const appnp_graph* g, const StepArgs& a, int epi,
-                            const float* z_rem, float* acc, const float* h_rem, int64_t ld_h,
-                            float* out, int64_t ld_out, int nv, hipStream_t s);
+                            const float* z_rem, const float* h_rem, int64_t ld_h, float* out,
+                            int64_t ld_out, int nv, int32_t* done, int iter, hipStream_t s);
 hipError_t launch_split_copy(const float* h, int64_t ld_h, int64_t n, int64_t f, int64_t fs,
                              float* main, float* rem, hipStream_t s);
 

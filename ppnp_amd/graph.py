@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import ctypes as C
 import itertools
+import warnings
 import weakref
 
 import numpy as np
@@ -117,7 +118,11 @@ class Graph:
                 1 if split_local else 0, C.c_void_p(_stream_ptr(device)), C.byref(out),
             )
         _lib.check("appnp_graph_create", rc)
-        return cls(out, device)
+        g = cls(out, device)
+        if source_blocks and g.source_block_bytes() == 0:
+            warnings.warn(f"ppnp_amd: the source-blocked copy of A_hat (n={n}) could not be "
+                          "built; this graph gathers whole rows", RuntimeWarning, stacklevel=2)
+        return g
 
     @classmethod
     def from_scipy(cls, adj, mode="sym", device=None, **kw):
@@ -147,6 +152,13 @@ class Graph:
         _lib.check("appnp_propagate_split_point",
                    _lib.load().appnp_propagate_split_point(self._h, int(f), dt, C.byref(fs)))
         return fs.value
+
+    def source_block_bytes(self) -> int:
+        """Device bytes of the source-blocked copy of A_hat (0: not built)."""
+        b = C.c_int64()
+        _lib.check("appnp_graph_source_blocks",
+                   _lib.load().appnp_graph_source_blocks(self._h, C.byref(b)))
+        return b.value
 
     def csr(self):
         """(row_ptr int32, col int32, val fp32, dinv fp64) as new device tensors."""

@@ -206,3 +206,31 @@ def test_split_adjoint_matches_oracle(graphs, ahat, f, K, p):
     close_fp32(dH.double().cpu().numpy(), plain.double().cpu().numpy())
     again = ppnp_amd.propagate_backward(graphs[0], dZ.to(DEV), K, 0.1, p_drop=p, seed=9)
     assert torch.equal(dH, again)
+
+
+def test_split_multi_pass_graph():
+    """More rows than one persistent launch holds in LDS (CUs x 16 waves x 640 rows: 2.6 M on
+    MI355X): the remainder pass sweeps the source blocks once per pass of row groups.  A
+    3 M-node graph, F = 36 (32 + 4), K = 2, against the float64 oracle; run-to-run bitwise."""
+    import ppnp_amd
+
+    n = 3_000_000
+    a = O.synth_graph(n, 3_000_000, seed=17)
+    G = ppnp_amd.Graph.from_scipy(a, device=DEV, features=36)
+    assert G.split_point(36) == 32 and G.source_block_bytes() > 0
+    H = torch.randn(n, 36, generator=torch.Generator().manual_seed(18))
+    Z = ppnp_amd.propagate_forward(G, H.to(DEV), 2, 0.1)
+    close_fp32(Z.double().cpu().numpy(), O.appnp_propagate(O.calc_a_hat(a, "sym"), H.numpy(), 2,
+                                                           0.1))
+    assert torch.equal(Z, ppnp_amd.propagate_forward(G, H.to(DEV), 2, 0.1))
+
+
+def test_source_blocks_only_when_requested():
+    """the regrouped copy costs ~8 B per nonzero, so it is built only for a feature
+    width that takes the split path (or on explicit request)."""
+    import ppnp_amd
+
+    a = O.synth_graph(70_000, 140_000, seed=19)
+    assert ppnp_amd.Graph.from_scipy(a, device=DEV).source_block_bytes() == 0
+    assert ppnp_amd.Graph.from_scipy(a, device=DEV, features=7).source_block_bytes() == 0
+    assert ppnp_amd.Graph.from_scipy(a, device=DEV, features=100).source_block_bytes() > 0
