@@ -268,7 +268,7 @@ __global__ __launch_bounds__(kBlock) void k_rb_walk(const int32_t* __restrict__ 
       if constexpr (FILL) {
         if (act) {
           const int32_t pos = base + (lane - head);
-          ent[pos] = ((uint32_t)(i - r0) << kRemColBits) | ((uint32_t)c & ((1u << kRemColBits) - 1u));
+          ent[pos] = ((uint32_t)(i - r0) << kRemColBits) | ((uint32_t)c & ((1u << br_log2) - 1u));
           bval[pos] = val[e];
         }
       } else {
