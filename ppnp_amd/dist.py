@@ -484,8 +484,9 @@ def rank_bytes(layout: Layout, n: int, f: int, nnz_hat: int, elem_bytes: int = 4
                overlap: bool = False) -> int:
     """Device bytes one rank of ``layout`` holds for the K loop (upper estimate): its rows'
     CSR (int32 row_ptr, int32 col + fp32 val; doubled by the local/remote split of overlap
-    mode), dinv (fp64, all n), the H slab of its rows, two full-height Z slabs, and the fp32
-    partial of overlap mode."""
+    mode; plus the source-blocked copy where a column slab takes the split-row path), dinv
+    (fp64, all n), the H slab of its rows, two full-height Z slabs, and the fp32 partial of
+    overlap mode."""
     R, C = layout.rows, layout.cols
     shard = -(-n // R)
     nnz_r = -(-nnz_hat // R)
@@ -494,6 +495,11 @@ def rank_bytes(layout: Layout, n: int, f: int, nnz_hat: int, elem_bytes: int = 4
     csr = 4 * (shard + 1) + 8 * nnz_r
     if overlap:
         csr += 4 * 2 * (shard + 1) + 8 * nnz_r
+    if R == 1 and elem_bytes == 4 and n > (1 << 16) and 32 < width <= 256 and width % 32 in (
+            1, 2, 3, 4):
+        # a column slab that takes the split-row path keeps the source-blocked copy of A_hat
+        # (8 B per nonzero plus one int per 2^16-row block and 640-row group: appnp_blocks.hip)
+        csr += 8 * nnz_hat + 4 * (-(-n // (1 << 16))) * (-(-n // 640) + 1)
     dense = (shard + 2 * shard * R) * ld * elem_bytes + (shard * ld * 4 if overlap else 0)
     return csr + 8 * n + dense
 

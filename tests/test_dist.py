@@ -155,6 +155,9 @@ def test_layout_memory_and_index_limits():
     assert min(shares, key=shares.get) == Layout(2, 4)
     assert choose_layout(8, n, 100, nnz, 4, int(1.45 * gb)) == Layout(2, 4)
     assert choose_layout(8, n, 100, nnz, 4, gb // 2) == Layout(2, 4)  # nothing fits: smallest
+    # a slab on the split-row path also holds the source-blocked copy of A_hat
+    assert rank_bytes(Layout(1, 1), n, 100, nnz) - rank_bytes(Layout(1, 1), n, 96, nnz) >= 8 * nnz
+    assert rank_bytes(Layout(1, 1), n, 100, nnz, elem_bytes=2) < rank_bytes(Layout(1, 1), n, 96, nnz)
 
 
 @pytest.mark.parametrize("spec,world", [("2x4", 8), ("4x2", 8), ("2x2", 4), ("2x3", 6)])
