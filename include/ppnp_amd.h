@@ -64,7 +64,7 @@ enum appnp_norm { APPNP_NORM_SYM = 0, APPNP_NORM_RW = 1 };
  * with F = 32q + r (e.g. F = 100) out of the random gather and forms their product in one
  * persistent, L2-resident pass per iteration, so a gathered row costs q cache lines instead
  * of q + 1.  Costs 8 bytes per nonzero plus one int32 per (block, 640-row group) of device
- * memory.  Best-effort: when the copy cannot be built (too many blocks, device memory), the
+ * memory (segments padded to 64 entries).  Best-effort: when the copy cannot be built (too many blocks, device memory), the
  * graph is still created and gathers whole rows; appnp_graph_source_blocks tells. */
 #define APPNP_GRAPH_SOURCE_BLOCKS 0x200
 
@@ -162,8 +162,7 @@ int appnp_graph_dinv(const appnp_graph* g, const double** dinv);
 
 /* Bytes of workspace appnp_propagate / appnp_propagate_bwd need for this shape.  The
  * workspace holds the ping-pong iterates with its own line-aligned leading dimension
- * (`ld` is accepted for ABI stability and ignored), and, on a graph with source blocks, the
- * remainder pass's pacing counters (zeroed by each call). */
+ * (`ld` is accepted for ABI stability and ignored). */
 size_t appnp_workspace_bytes(const appnp_graph* g, int64_t f, int64_t ld, int dtype);
 
 /* The column split appnp_propagate uses for this shape when H, Z and the workspace are 16-B

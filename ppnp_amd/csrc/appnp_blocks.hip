@@ -11,8 +11,11 @@
 //   * The remainder product  R = (M_k o A_hat) Z_rem  runs as ONE launch per iteration that
 //     sweeps A_hat by SOURCE block: block b holds the entries whose column lies in
 //     [b * 2^16, (b+1) * 2^16), i.e. 1 MB of Z_rem, which sits in every XCD's 4 MB L2 while
-//     the chip gathers from it.  All workgroups walk the blocks in the same order, paced so
-//     that none runs more than one block ahead of the slowest: at most two blocks are live.
+//     the chip gathers from it.  Every wave walks the blocks in the same order at about the
+//     same rate, so the blocks live in L2 at one time are the few between the slowest and
+//     the fastest wave.  (Pacing the workgroups with per-block counters and a barrier kept
+//     that window at two blocks but drained each wave's pipeline at every block: 8.33 against
+//     8.15 ms per products-synth iteration without it.)
 //
 // The accumulators never leave the chip.  The launch is persistent -- one 1024-thread
 // workgroup per CU, each of its 16 waves owning a group of <= 640 destination rows whose
@@ -21,16 +24,20 @@
 // HBM every launch: 19 launches and ~2.7 GB of streams per products-synth iteration.)
 //
 // Work inside a wave is entry-parallel, so hub rows and ragged groups cost no idle lanes:
-// the wave streams its segment of entries (block b, its group) 64 at a time -- one entry per
-// lane, sorted by (row, column) -- gathers Z_rem[column] from L2, and combines the products
+// the wave streams its entries -- block after block, one contiguous run per wave, each
+// block's segment padded to whole chunks of 64 so a chunk never mixes blocks -- one entry per
+// lane, sorted by (row, column); gathers Z_rem[column] from L2; and combines the products
 // of equal rows with a segmented inclusive scan over the lanes (DPP row shifts + row
 // broadcasts, fixed order); each segment's last lane adds the sum into its row's LDS slot.
-// The order of every addition is fixed by the layout: bitwise deterministic run to run.
+// U = 8 chunks (512 entries) are in flight per wave: the pass is bound by the latency of the
+// entry load followed by the dependent L2 gather, not by bandwidth.  The order of every
+// addition is fixed by the layout: bitwise deterministic run to run.
 //
-// The regrouped copy of A_hat (APPNP_GRAPH_SOURCE_BLOCKS) is built at graph creation: entries
-// of segment (pass, block, group) are contiguous, packed as (row in group << 20 | column in
-// block) with their fp32 value; rb_off holds one start per segment -- passes x blocks x
-// (CUs x 16) ints, linear in n (one int per 2^16 x 640 tile of A_hat, ~0.6 MB on products).
+// The regrouped copy of A_hat (APPNP_GRAPH_SOURCE_BLOCKS) is built at graph creation: the
+// entries of wave group g's block b are the segment off[g * nb + b] .. off[g * nb + b + 1],
+// packed as (row in group << 20 | column in block) with their fp32 value; padding entries are
+// all ones with value 0.  off holds passes x (CUs x 16) x blocks + 1 ints: linear in n
+// (one int per 640-row x 2^16-column tile of A_hat, ~0.6 MB on products-synth).
 #include <algorithm>
 #include <cstdlib>
 
@@ -46,19 +53,18 @@ constexpr int kRemMaxRg = kRemLdsBytes / (kRemWaves * 16);  // 640 rows per wave
 constexpr uint32_t kRemNone = 0xffffffffu;      // packed entry of an idle lane (row 4095)
 constexpr int kWalkWaves = kWavesPerBlock;      // build walk: one wave per group
 constexpr int kWalkMaxBlocks = 4096;            // LDS cursors of the build walk: 64 KiB
-constexpr int kPaceSpins = 2048;                // bounded pacing wait (then run free)
+constexpr int kRemChunk = kWave;                // entries per chunk; segments padded to it
+constexpr int kRemU = 8;                        // chunks in flight per wave
 
 static_assert(kRemMaxRg < (1 << kRemRowBits), "row in group must fit the packed entry");
 static_assert(kRemRowBits + kRemColBits == 32, "packed entry is 32 bits");
 
 struct RemLayout {
-  const int32_t* off;   // segment starts
-  const uint32_t* ent;  // packed (row in group, column in block)
+  const int32_t* off;   // segment starts, [(pass * slots + slot) * nb + block]
+  const uint32_t* ent;  // packed (row in group, column in block); padding: kRemNone
   const float* val;
-  int32_t* done;        // [passes * nb] blocks finished, cumulative over the call's iterations
+  const int32_t* cblk;  // source block of each chunk of 64 entries
   int32_t nb, br_log2, slots, rg, passes;
-  int32_t iter;         // index of this launch within the call (pacing target)
-  int32_t pace;         // 0: no pacing
 };
 
 // ---- segmented inclusive scan over the 64 lanes (rows non-decreasing across lanes) --------
@@ -95,20 +101,6 @@ __device__ __forceinline__ void seg_scan(int row, f32x4& v) {
   seg_step<kDppRowShr8, 0xf>(row, v);
   seg_step<kDppRowBcast15, 0xa>(row, v);  // rows 1, 3 <- lanes 15, 47
   seg_step<kDppRowBcast31, 0xc>(row, v);  // rows 2, 3 <- lane 31
-}
-
-// Wait (one lane) until every workgroup has finished block b - 2 of this iteration, so the
-// chip gathers from at most two blocks at once.  Bounded: on a timeout the caller stops
-// pacing for the rest of the launch (the result never depends on the pacing, only the L2 hit
-// rate does; a grid larger than the resident set can therefore not deadlock).
-__device__ __forceinline__ bool pace_wait(int32_t* ctr, int target) {
-  __attribute__((address_space(1))) int32_t* c =
-      (__attribute__((address_space(1))) int32_t*)ctr;
-  for (int spin = 0; spin < kPaceSpins; ++spin) {
-    if (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return true;
-    __builtin_amdgcn_s_sleep(4);
-  }
-  return false;
 }
 
 // Epilogue of one row of the iteration: FWD out[i, :nv] = (1-alpha) R[i] + alpha H_rem[i]
@@ -168,73 +160,69 @@ __global__ __launch_bounds__(kRemThreads) void k_rem_persist(StepArgs a, RemLayo
   const f32x4* __restrict__ z = static_cast<const f32x4*>(a.zin);
   const int64_t slot = (int64_t)blockIdx.x * kRemWaves + wv;
   const uint32_t cmask = (1u << kRemColBits) - 1u;
-  const int target = (L.iter + 1) * (int)gridDim.x;
-  bool pacing = L.pace != 0;
   for (int p = 0; p < L.passes; ++p) {
-    const int64_t r0 = ((int64_t)p * L.slots + slot) * L.rg;
+    const int64_t g = (int64_t)p * L.slots + slot;
+    const int64_t r0 = g * L.rg;
     const int rows = (int)max<int64_t>(0, min<int64_t>(L.rg, a.n_rows - r0));
     for (int r = lane; r < rows; r += kWave) acc[r] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    int32_t* done = L.done + (int64_t)p * L.nb;
-    for (int b = 0; b < L.nb; ++b) {
-      if (b >= 2 && threadIdx.x == 0 && pacing) pacing = pace_wait(done + b - 2, target);
-      __syncthreads();
-      const int64_t sg = ((int64_t)p * L.nb + b) * L.slots + slot;
-      const int32_t beg = L.off[sg], end = L.off[sg + 1];
-      const int64_t cbase = (int64_t)b << L.br_log2;
-      for (int32_t c0 = beg; c0 < end; c0 += kWave * U) {
-        uint32_t en[U];
-        float wt[U];
-        f32x4 zv[U];
+    // this wave's stream: blocks 0..nb-1 back to back, each a whole number of chunks; the
+    // block of chunk c is cblk[c]
+    const int32_t c_end = L.off[(g + 1) * L.nb] / kRemChunk;
+    for (int32_t c = L.off[g * L.nb] / kRemChunk; c < c_end; c += U) {
+      const int nch = min(U, c_end - c);
+      int64_t cbase[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int32_t e = c0 + u * kWave + lane;
-          en[u] = kRemNone;
-          wt[u] = 0.0f;
-          if (e < end) {
-            en[u] = ld_nt<uint32_t>(L.ent + e);
-            wt[u] = ld_nt<float>(L.val + e);
-          }
-        }
+      for (int u = 0; u < U; ++u)
+        cbase[u] = u < nch ? (int64_t)L.cblk[c + u] << L.br_log2 : 0;
+      uint32_t en[U];
+      float wt[U];
+      f32x4 zv[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u)
-          zv[u] = en[u] != kRemNone ? z[cbase + (en[u] & cmask)] : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          if (c0 + u * kWave >= end) break;  // wave-uniform
-          const bool act = en[u] != kRemNone;
-          const int row = (int)(en[u] >> kRemColBits);
-          const float w =
-              act ? edge_weight(wt[u], r0 + row, (int32_t)(cbase + (en[u] & cmask)), a) : 0.0f;
-          f32x4 v = f32x4{w * zv[u].x, w * zv[u].y, w * zv[u].z, w * zv[u].w};
-          seg_scan(row, v);
-          const int prev = __shfl_up(row, 1);
-          const unsigned long long heads = __ballot(lane == 0 || prev != row);
-          const bool tail = lane == kWave - 1 || ((heads >> (lane + 1)) & 1ull);
-          if (act && tail) {
-            const f32x4 c = acc[row];
-            acc[row] = f32x4{c.x + v.x, c.y + v.y, c.z + v.z, c.w + v.w};
-          }
+      for (int u = 0; u < U; ++u) {
+        en[u] = kRemNone;
+        wt[u] = 0.0f;
+        if (u < nch) {
+          const int64_t e = (int64_t)(c + u) * kRemChunk + lane;
+          en[u] = ld_nt<uint32_t>(L.ent + e);
+          wt[u] = ld_nt<float>(L.val + e);
         }
       }
-      __syncthreads();
-      if (threadIdx.x == 0 && L.pace)
-        __hip_atomic_fetch_add((__attribute__((address_space(1))) int32_t*)(done + b), 1,
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        zv[u] = en[u] != kRemNone ? z[cbase[u] + (en[u] & cmask)] : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (u >= nch) break;  // wave-uniform
+        const bool act = en[u] != kRemNone;
+        const int row = (int)(en[u] >> kRemColBits);
+        const float w =
+            act ? edge_weight(wt[u], r0 + row, (int32_t)(cbase[u] + (en[u] & cmask)), a) : 0.0f;
+        f32x4 v = f32x4{w * zv[u].x, w * zv[u].y, w * zv[u].z, w * zv[u].w};
+        seg_scan(row, v);
+        const int prev = __shfl_up(row, 1);
+        const unsigned long long heads = __ballot(lane == 0 || prev != row);
+        const bool tail = lane == kWave - 1 || ((heads >> (lane + 1)) & 1ull);
+        if (act && tail) {
+          const f32x4 c = acc[row];
+          acc[row] = f32x4{c.x + v.x, c.y + v.y, c.z + v.z, c.w + v.w};
+        }
+      }
     }
     for (int r = lane; r < rows; r += kWave) rem_finish<EPI>(a, r0 + r, acc[r]);
   }
 }
 
 // Build walk: one wave per group, walking the group's rows in order with one cursor per
-// source block in LDS.  COUNT: the number of entries of each (pass, block, group) segment
-// into cnt, plus the off-diagonal entries within kNearRows of their row (gather locality).
-// FILL: cursors start at the segment offsets; every entry is written to its slot.  A row's
-// columns are sorted, so its entries of one block are a run of consecutive lanes.
+// source block in LDS.  COUNT: the number of entries of each (group, block) segment, padded
+// to whole chunks, into cnt, plus the off-diagonal entries within kNearRows of their row
+// (gather locality).  FILL: cursors start at the segment offsets; every entry is written to
+// its slot (the padding stays as preset).  A row's columns are sorted, so its entries of one
+// block are a run of consecutive lanes.
 template <bool FILL>
 __global__ __launch_bounds__(kBlock) void k_rb_walk(const int32_t* __restrict__ rp,
                                                     const int32_t* __restrict__ col,
                                                     const float* __restrict__ val, int64_t n,
-                                                    int rg, int slots, int nb, int br_log2,
+                                                    int rg, int nb, int br_log2,
                                                     int64_t n_groups, int32_t* __restrict__ cnt,
                                                     const int32_t* __restrict__ off,
                                                     uint32_t* __restrict__ ent,
@@ -246,8 +234,7 @@ __global__ __launch_bounds__(kBlock) void k_rb_walk(const int32_t* __restrict__ 
   int32_t* cur = walk_cur + (int64_t)w * nb;
   const int64_t g = (int64_t)blockIdx.x * kWalkWaves + w;
   if (g >= n_groups) return;  // no workgroup barrier in this kernel
-  const int64_t p = g / slots, s = g - p * slots;
-  for (int b = lane; b < nb; b += kWave) cur[b] = FILL ? off[(p * nb + b) * slots + s] : 0;
+  for (int b = lane; b < nb; b += kWave) cur[b] = FILL ? off[g * nb + b] : 0;
   const int64_t r0 = g * rg, r1 = min<int64_t>(n, r0 + rg);
   unsigned long long nr = 0;
   for (int64_t i = r0; i < r1; ++i) {
@@ -279,11 +266,22 @@ __global__ __launch_bounds__(kBlock) void k_rb_walk(const int32_t* __restrict__ 
     }
   }
   if constexpr (!FILL) {
-    for (int b = lane; b < nb; b += kWave) cnt[(p * nb + b) * slots + s] = cur[b];
+    for (int b = lane; b < nb; b += kWave)
+      cnt[g * nb + b] = (cur[b] + kRemChunk - 1) / kRemChunk * kRemChunk;
 #pragma unroll
     for (int o = 1; o < kWave; o <<= 1) nr += __shfl_xor(nr, o);
     if (lane == 0 && nr) atomicAdd(near, nr);
   }
+}
+
+// cblk[c] = b for every chunk c of segment (group, block b).  Thread per segment.
+__global__ __launch_bounds__(kBlock) void k_rb_chunks(const int32_t* __restrict__ off,
+                                                      int64_t cells, int nb,
+                                                      int32_t* __restrict__ cblk) {
+  const int64_t sg = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (sg >= cells) return;
+  const int b = (int)(sg % nb);
+  for (int32_t c = off[sg] / kRemChunk; c < off[sg + 1] / kRemChunk; ++c) cblk[c] = b;
 }
 
 // H [n, ld_h] -> the split layout: main [n, fs] (whole lines per row) and rem [n, 4]
@@ -324,12 +322,11 @@ __global__ __launch_bounds__(kBlock) void k_split_copy(const float* __restrict__
 template <int EPI>
 hipError_t launch_rem(dim3 grid, dim3 block, size_t lds, hipStream_t s, const StepArgs& a,
                       const RemLayout& L) {
-  constexpr int kU = 2;  // chunks of 64 entries in flight per wave
   static const hipError_t attr = hipFuncSetAttribute(  // > 64 KiB of dynamic LDS, once
-      reinterpret_cast<const void*>(k_rem_persist<EPI, kU>),
+      reinterpret_cast<const void*>(k_rem_persist<EPI, kRemU>),
       hipFuncAttributeMaxDynamicSharedMemorySize, kRemLdsBytes);
   if (attr != hipSuccess) return attr;
-  hipLaunchKernelGGL((k_rem_persist<EPI, kU>), grid, block, lds, s, a, L);
+  hipLaunchKernelGGL((k_rem_persist<EPI, kRemU>), grid, block, lds, s, a, L);
   return hipGetLastError();
 }
 
@@ -377,28 +374,36 @@ int graph_build_source_blocks(appnp_graph* g, hipStream_t s) {
   const int64_t n_groups = passes * slots;
   const unsigned grid = (unsigned)((n_groups + kWalkWaves - 1) / kWalkWaves);
   const size_t lds = (size_t)kWalkWaves * nb * sizeof(int32_t);
-  const int64_t nnz = std::max<int64_t>(1, g->nnz_hat);
+  int64_t h_tot[2] = {0, 0};  // padded entries, near entries
   if (ok(hipMalloc(&g->rb_off, (cells + 1) * sizeof(int32_t))) &&
-      ok(hipMalloc(&g->rb_ent, nnz * sizeof(uint32_t))) &&
-      ok(hipMalloc(&g->rb_val, nnz * sizeof(float))) &&
       ok(hipMalloc(&cnt, cells * sizeof(int32_t))) &&
       ok(hipMalloc(&bsum, scan_partials(cells) * sizeof(int64_t))) &&
       ok(hipMalloc(&tot, 2 * sizeof(int64_t))) &&
       ok(hipMemsetAsync(tot, 0, 2 * sizeof(int64_t), s))) {
     hipLaunchKernelGGL(k_rb_walk<false>, dim3(grid), dim3(kBlock), lds, s, g->row_ptr, g->col,
-                       g->val, rows, (int)rg, (int)slots, (int)nb, br_log2, n_groups, cnt,
-                       nullptr, nullptr, nullptr, reinterpret_cast<unsigned long long*>(tot + 1));
-    if (ok(hipGetLastError()) && ok(exclusive_scan(cnt, cells, g->rb_off, bsum, tot, s))) {
-      hipLaunchKernelGGL(k_rb_walk<true>, dim3(grid), dim3(kBlock), lds, s, g->row_ptr, g->col,
-                         g->val, rows, (int)rg, (int)slots, (int)nb, br_log2, n_groups, nullptr,
-                         g->rb_off, g->rb_ent, g->rb_val, nullptr);
-      ok(hipGetLastError());
+                       g->val, rows, (int)rg, (int)nb, br_log2, n_groups, cnt, nullptr, nullptr,
+                       nullptr, reinterpret_cast<unsigned long long*>(tot + 1));
+    if (ok(hipGetLastError()) && ok(exclusive_scan(cnt, cells, g->rb_off, bsum, tot, s)) &&
+        ok(hipMemcpyAsync(h_tot, tot, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, s)) &&
+        ok(hipStreamSynchronize(s))) {
+      // padded total: the int32 segment offsets must hold it
+      if (h_tot[0] > INT32_MAX) rc = APPNP_ERANGE;
     }
-    int64_t near = 0;
-    if (rc == APPNP_OK)
-      ok(hipMemcpyAsync(&near, tot + 1, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-    if (rc == APPNP_OK && ok(hipStreamSynchronize(s)))
-      g->near_frac = g->nnz_hat > 0 ? (double)near / (double)g->nnz_hat : 0.0;
+    const int64_t total = std::max<int64_t>(1, h_tot[0]);
+    if (rc == APPNP_OK && ok(hipMalloc(&g->rb_ent, total * sizeof(uint32_t))) &&
+        ok(hipMalloc(&g->rb_val, total * sizeof(float))) &&
+        ok(hipMemsetAsync(g->rb_ent, 0xff, total * sizeof(uint32_t), s)) &&  // kRemNone
+        ok(hipMemsetAsync(g->rb_val, 0, total * sizeof(float), s)) &&
+        ok(hipMalloc(&g->rb_cblk, std::max<int64_t>(1, total / kRemChunk) * sizeof(int32_t)))) {
+      hipLaunchKernelGGL(k_rb_walk<true>, dim3(grid), dim3(kBlock), lds, s, g->row_ptr, g->col,
+                         g->val, rows, (int)rg, (int)nb, br_log2, n_groups, nullptr, g->rb_off,
+                         g->rb_ent, g->rb_val, nullptr);
+      if (ok(hipGetLastError()))
+        hipLaunchKernelGGL(k_rb_chunks, dim3((unsigned)((cells + kBlock - 1) / kBlock)),
+                           dim3(kBlock), 0, s, g->rb_off, cells, (int)nb, g->rb_cblk);
+      if (ok(hipGetLastError()) && ok(hipStreamSynchronize(s)))
+        g->near_frac = g->nnz_hat > 0 ? (double)h_tot[1] / (double)g->nnz_hat : 0.0;
+    }
   }
   if (cnt) (void)hipFree(cnt);
   if (bsum) (void)hipFree(bsum);
@@ -407,11 +412,14 @@ int graph_build_source_blocks(appnp_graph* g, hipStream_t s) {
     if (g->rb_off) (void)hipFree(g->rb_off);
     if (g->rb_ent) (void)hipFree(g->rb_ent);
     if (g->rb_val) (void)hipFree(g->rb_val);
+    if (g->rb_cblk) (void)hipFree(g->rb_cblk);
     g->rb_off = nullptr;
     g->rb_ent = nullptr;
     g->rb_val = nullptr;
+    g->rb_cblk = nullptr;
     return rc;
   }
+  g->rb_total = h_tot[0];
   g->rb_nb = (int32_t)nb;
   g->rb_br_log2 = br_log2;
   g->rb_grid = cus;
@@ -421,22 +429,14 @@ int graph_build_source_blocks(appnp_graph* g, hipStream_t s) {
   return APPNP_OK;
 }
 
-// Pacing counters of one call (passes x blocks int32), zeroed by the caller once per call.
-size_t remainder_counter_bytes(const appnp_graph* g) {
-  if (!g->rb_off) return 0;
-  return ((size_t)g->rb_passes * g->rb_nb * sizeof(int32_t) + 255) / 256 * 256;
-}
-
 // One iteration of the remainder columns: R = (M_k o A_hat) Z_rem over all source blocks in
 // one persistent launch (k_rem_persist), epilogue included.  a: the iteration's StepArgs
 // (dropout key, n_rows, scale, alpha); z_rem [n, 4]; h_rem = H + fs; out / ld_out / nv: where
 // the nv valid columns of Z_{k+1} go.  epi = EPI_BWD (adjoint): h_rem / ld_h are dH's
-// remainder columns, accumulated into; out (G_k's remainder) may be null.  done: the call's
-// pacing counters (remainder_counter_bytes, zeroed before the first iteration); iter: the
-// launch's index within the call.
+// remainder columns, accumulated into; out (G_k's remainder) may be null.
 hipError_t launch_remainder(const appnp_graph* g, const StepArgs& a_in, int epi,
                             const float* z_rem, const float* h_rem, int64_t ld_h, float* out,
-                            int64_t ld_out, int nv, int32_t* done, int iter, hipStream_t s) {
+                            int64_t ld_out, int nv, hipStream_t s) {
   StepArgs a = a_in;
   a.zin = z_rem;
   a.aux = nullptr;
@@ -452,10 +452,8 @@ hipError_t launch_remainder(const appnp_graph* g, const StepArgs& a_in, int epi,
   a.ld_out = ld_out;
   a.f = nv;
   if (a.n_rows <= 0) return hipSuccess;
-  // APPNP_REM_PACE=0 (measurement): no pacing between the workgroups
-  static const int pace = env_or("APPNP_REM_PACE", 1);
-  RemLayout L{g->rb_off, g->rb_ent, g->rb_val, done, g->rb_nb, g->rb_br_log2, g->rb_slots,
-              g->rb_rg, g->rb_passes, iter, pace && done ? 1 : 0};
+  RemLayout L{g->rb_off, g->rb_ent, g->rb_val, g->rb_cblk, g->rb_nb, g->rb_br_log2, g->rb_slots, g->rb_rg,
+              g->rb_passes};
   const size_t lds = (size_t)kRemWaves * g->rb_rg * sizeof(f32x4);
   const dim3 grid((unsigned)g->rb_grid), block(kRemThreads);
   if (epi == EPI_BWD) return launch_rem<EPI_BWD>(grid, block, lds, s, a, L);

@@ -312,7 +312,7 @@ void graph_free(appnp_graph* g) {
   if (!g) return;
   void* ptrs[] = {g->row_ptr, g->col, g->val, g->lrow_ptr, g->lcol, g->lval,
                   g->rrow_ptr, g->rcol, g->rval, g->dinv, g->t_row_ptr, g->t_col, g->t_val,
-                  g->heavy, g->t_heavy, g->hub, g->t_hub, g->rb_off, g->rb_ent, g->rb_val};
+                  g->heavy, g->t_heavy, g->hub, g->t_hub, g->rb_off, g->rb_ent, g->rb_val, g->rb_cblk};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   g->row_ptr = g->col = g->lrow_ptr = g->lcol = g->rrow_ptr = g->rcol = nullptr;
@@ -324,7 +324,9 @@ void graph_free(appnp_graph* g) {
   g->rb_off = nullptr;
   g->rb_ent = nullptr;
   g->rb_val = nullptr;
+  g->rb_cblk = nullptr;
   g->rb_nb = g->rb_passes = 0;
+  g->rb_total = 0;
 }
 
 #define APPNP_TRY(expr)                                                         \

@@ -38,11 +38,13 @@ struct appnp_graph {
   int32_t* t_col = nullptr;
   float* t_val = nullptr;
   // A_hat regrouped for the persistent remainder pass (APPNP_GRAPH_SOURCE_BLOCKS,
-  // appnp_blocks.hip): segment (pass, source block, group) holds the entries of one wave's
-  // group of rows whose column lies in that block, sorted by (row, column)
-  int32_t* rb_off = nullptr;    // [rb_passes * rb_nb * rb_slots + 1] segment starts
-  uint32_t* rb_ent = nullptr;   // [nnz_hat] (row in group << kRemColBits) | column in block
-  float* rb_val = nullptr;      // [nnz_hat]
+  // appnp_blocks.hip): segment (group, source block) holds the entries of one wave's group of
+  // rows whose column lies in that block, sorted by (row, column), padded to 64 entries
+  int32_t* rb_off = nullptr;    // [rb_passes * rb_slots * rb_nb + 1] segment starts
+  uint32_t* rb_ent = nullptr;   // [rb_total] (row in group << kRemColBits) | column in block
+  float* rb_val = nullptr;      // [rb_total]
+  int32_t* rb_cblk = nullptr;   // [rb_total / 64] source block of each chunk of 64 entries
+  int64_t rb_total = 0;         // entries including the padding
   int32_t rb_nb = 0;            // source blocks of 2^rb_br_log2 rows
   int32_t rb_br_log2 = 0;
   int32_t rb_grid = 0;          // workgroups of the pass (one per CU)
@@ -75,10 +77,9 @@ hipError_t exclusive_scan(const int32_t* cnt, int64_t rows, int32_t* out, int64_
 
 // appnp_blocks.hip
 int graph_build_source_blocks(appnp_graph* g, hipStream_t s);
-size_t remainder_counter_bytes(const appnp_graph* g);
 hipError_t launch_remainder(const appnp_graph* g, const StepArgs& a, int epi,
                             const float* z_rem, const float* h_rem, int64_t ld_h, float* out,
-                            int64_t ld_out, int nv, int32_t* done, int iter, hipStream_t s);
+                            int64_t ld_out, int nv, hipStream_t s);
 hipError_t launch_split_copy(const float* h, int64_t ld_h, int64_t n, int64_t f, int64_t fs,
                              float* main, float* rem, hipStream_t s);
 
