@@ -59,7 +59,7 @@ enum appnp_norm { APPNP_NORM_SYM = 0, APPNP_NORM_RW = 1 };
  * for 'sym' on an undirected graph, where A_hat^T == A_hat. */
 #define APPNP_GRAPH_TRANSPOSE 0x100
 
-/* OR into `mode`: also keep a copy of A_hat regrouped by source block (2^16 source rows per
+/* OR into `mode`: also keep a copy of A_hat regrouped by source block (2^15 source rows per
  * block; full graphs only).  appnp_propagate then takes the last 1-4 columns of fp32 rows
  * with F = 32q + r (e.g. F = 100) out of the random gather and forms their product in one
  * persistent, L2-resident pass per iteration, so a gathered row costs q cache lines instead

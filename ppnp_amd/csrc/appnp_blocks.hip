@@ -10,7 +10,7 @@
 //     gather is exactly q lines) and Z_rem [n, 4] (16 B per row).
 //   * The remainder product  R = (M_k o A_hat) Z_rem  runs as ONE launch per iteration that
 //     sweeps A_hat by SOURCE block: block b holds the entries whose column lies in
-//     [b * 2^16, (b+1) * 2^16), i.e. 1 MB of Z_rem, which sits in every XCD's 4 MB L2 while
+//     [b * 2^15, (b+1) * 2^15), i.e. 512 KB of Z_rem, which sits in every XCD's 4 MB L2 while
 //     the chip gathers from it.  Every wave walks the blocks in the same order at about the
 //     same rate, so the blocks live in L2 at one time are the few between the slowest and
 //     the fastest wave.  (Pacing the workgroups with per-block counters and a barrier kept
@@ -37,7 +37,7 @@
 // entries of wave group g's block b are the segment off[g * nb + b] .. off[g * nb + b + 1],
 // packed as (row in group << 20 | column in block) with their fp32 value; padding entries are
 // all ones with value 0.  off holds passes x (CUs x 16) x blocks + 1 ints: linear in n
-// (one int per 640-row x 2^16-column tile of A_hat, ~0.6 MB on products-synth).
+// (one int per 640-row x 2^15-column tile of A_hat, ~1.2 MB on products-synth).
 #include <algorithm>
 #include <cstdlib>
 

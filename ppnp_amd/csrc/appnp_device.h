@@ -56,8 +56,11 @@ struct StepArgs {
 constexpr int kHeavyRow = 32;   // a row longer than this gets a whole wavefront (narrow)
 constexpr int kHubRow = 512;    // ... and one longer than this is dispatched first (wide)
 constexpr int kWideAvgRow = 24; // mean row length from which large graphs take a wave per row
-constexpr int kSourceBlockLog2 = 16;  // source rows per block of the remainder pass: 2^16
-                                     // (1 MB of 16-B remainders; two blocks stay in L2)
+constexpr int kSourceBlockLog2 = 15;  // source rows per block of the remainder pass: 2^15
+                                     // (512 KB of 16-B remainders; the waves of an XCD drift
+                                     // over a few blocks, which must share its 4 MB L2:
+                                     // products-synth 2^14 / 2^15 / 2^16 / 2^17 rows
+                                     // 8.00 / 7.97 / 8.22 / 8.27 ms per iteration)
 constexpr int kRemWaves = 16;        // waves per workgroup of the persistent remainder pass
 constexpr int kRemColBits = 20;      // column-in-block bits of a packed remainder entry
 constexpr int kRemRowBits = 12;      // row-in-group bits (the rest of the 32)

@@ -498,8 +498,8 @@ def rank_bytes(layout: Layout, n: int, f: int, nnz_hat: int, elem_bytes: int = 4
     if R == 1 and elem_bytes == 4 and n > (1 << 16) and 32 < width <= 256 and width % 32 in (
             1, 2, 3, 4):
         # a column slab that takes the split-row path keeps the source-blocked copy of A_hat
-        # (8 B per nonzero plus one int per 2^16-row block and 640-row group: appnp_blocks.hip)
-        csr += 8 * nnz_hat + 4 * (-(-n // (1 << 16))) * (-(-n // 640) + 1)
+        # (8 B per nonzero plus one int per 2^15-row block and 640-row group: appnp_blocks.hip)
+        csr += 9 * nnz_hat + 4 * (-(-n // (1 << 15))) * (-(-n // 640) + 1)
     dense = (shard + 2 * shard * R) * ld * elem_bytes + (shard * ld * 4 if overlap else 0)
     return csr + 8 * n + dense
 
