@@ -1,12 +1,22 @@
-// launch_probe.hip -- microbenchmark: per-launch floor of back-to-back dependent kernels on
-// MI355X (empty kernels, and kernels with a chain of D dependent global loads), by grid size.
-// Design input for the latency regime of the APPNP step (small graphs).  Not part of the library.
+// launch_probe.hip -- microbenchmark of the latency regime (small graphs).
+// Not part of the library.
 //
 //   hipcc -O3 --offload-arch=gfx950 tools/launch_probe.hip -o tools/bin/launch_probe
+//
+// 1. Per-launch time of back-to-back dependent kernels, eager (host submission included) and
+//    replayed from a captured hipGraph (device-side boundary only), by grid size.
+// 2. Per-barrier time of a grid barrier inside one persistent launch (one chip-wide arrival
+//    counter, agent-scope atomics, release/acquire fences; bounded spins).
+// 3. A PubMed-sized APPNP K-loop (19,717 nodes, 44,324 undirected random edges + self loops,
+//    F = 3, K = 10, one G = 4-lane group per row, 4 entries in flight): K captured launches
+//    against ONE persistent launch whose iterations are separated by the grid barrier.
+//    Both write the same Z (checked bitwise).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <vector>
 
 #define CHECK(x)                                                                     \
   do {                                                                               \
@@ -17,55 +27,242 @@
     }                                                                                \
   } while (0)
 
+typedef __attribute__((address_space(1))) unsigned gu32;
+
 __global__ void k_empty(int* p) {
   if (p && threadIdx.x == 1023) p[0] = 0;
 }
 
-// D dependent loads per thread through a pointer-chasing table (next = tab[cur]), then a store
-template <int D>
-__global__ __launch_bounds__(256) void k_chain(const int* __restrict__ tab, int* __restrict__ out,
-                                               int n) {
-  int i = (blockIdx.x * 256 + threadIdx.x) % n;
-#pragma unroll
-  for (int d = 0; d < D; ++d) i = tab[i];
-  out[blockIdx.x * 256 + threadIdx.x] = i;
-}
+hipStream_t g_stream;
 
 template <typename F>
-float per_launch_us(F launch, int reps = 200) {
+float time_us(F body, int reps) {
   hipEvent_t a, b;
   CHECK(hipEventCreate(&a));
   CHECK(hipEventCreate(&b));
-  for (int i = 0; i < 20; ++i) launch();
-  CHECK(hipEventRecord(a));
-  for (int i = 0; i < reps; ++i) launch();
-  CHECK(hipEventRecord(b));
+  for (int i = 0; i < 5; ++i) body();
+  CHECK(hipDeviceSynchronize());
+  CHECK(hipEventRecord(a, g_stream));
+  for (int i = 0; i < reps; ++i) body();
+  CHECK(hipEventRecord(b, g_stream));
   CHECK(hipEventSynchronize(b));
   float ms;
   CHECK(hipEventElapsedTime(&ms, a, b));
   return ms * 1e3f / reps;
 }
 
+// ---- grid barrier: one chip-wide arrival counter (agent-scope atomics), each workgroup waits
+// until gen * gridDim.x arrivals.  Generations continue across launches (gen0 = barriers
+// already passed), so nothing is reset between timed launches.  Bounded: a spin that runs out
+// sets *fail (reported) instead of hanging.
+__device__ __forceinline__ void grid_barrier(gu32* cnt, unsigned gen, gu32* fail) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains first
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned target = gen * gridDim.x;
+    unsigned spins = 0;
+    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1u << 16)) {
+        __hip_atomic_store(fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+}
+
+__global__ void k_barriers(gu32* cnt, int n_bar, gu32* fail, unsigned gen0) {
+  for (int i = 1; i <= n_bar; ++i) grid_barrier(cnt, gen0 + i, fail);
+}
+
+// ---- one APPNP iteration, G = 4 lanes per row (F = 3: lane 3 idle), 4 entries in flight
+__device__ __forceinline__ void appnp_rows(const int* __restrict__ rp, const int* __restrict__ col,
+                                           const float* __restrict__ val,
+                                           const float* __restrict__ zin,
+                                           const float* __restrict__ h, float* __restrict__ zout,
+                                           int n, int f, float alpha, int row0, int stride) {
+  const int sub = threadIdx.x >> 2, gl = threadIdx.x & 3;
+  for (int row = row0 + sub; row < n; row += stride) {
+    const int beg = rp[row], end = rp[row + 1];
+    float acc = 0.0f;
+    for (int e = beg; e < end; e += 4) {
+      int c[4];
+      float w[4], z[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        c[u] = e + u < end ? col[e + u] : 0;
+        w[u] = e + u < end ? val[e + u] : 0.0f;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) z[u] = (e + u < end && gl < f) ? zin[(int64_t)c[u] * 4 + gl] : 0.0f;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc = fmaf(w[u], z[u], acc);
+    }
+    if (gl < f) zout[(int64_t)row * 4 + gl] = fmaf(alpha, h[(int64_t)row * 4 + gl], (1.0f - alpha) * acc);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_step(const int* rp, const int* col, const float* val,
+                                              const float* zin, const float* h, float* zout,
+                                              int n, int f, float alpha) {
+  appnp_rows(rp, col, val, zin, h, zout, n, f, alpha, blockIdx.x * 64, gridDim.x * 64);
+}
+
+__global__ __launch_bounds__(256) void k_loop(const int* rp, const int* col, const float* val,
+                                              const float* h, float* z0, float* z1, int n, int f,
+                                              float alpha, int K, gu32* cnt, gu32* fail,
+                                              unsigned gen0) {
+  const float* src = h;
+  for (int k = 0; k < K; ++k) {
+    float* dst = ((K - 1 - k) % 2 == 0) ? z0 : z1;
+    appnp_rows(rp, col, val, src, h, dst, n, f, alpha, blockIdx.x * 64, gridDim.x * 64);
+    if (k + 1 < K) grid_barrier(cnt, gen0 + k + 1, fail);
+    src = dst;
+  }
+}
+
 int main() {
-  const int n = 1 << 20;
-  int *tab, *out;
-  CHECK(hipMalloc(&tab, n * sizeof(int)));
-  CHECK(hipMalloc(&out, 4096 * 256 * sizeof(int)));
-  int* h = (int*)malloc(n * sizeof(int));
-  uint64_t s = 88172645463325252ull;
-  for (int i = 0; i < n; ++i) {
-    s ^= s << 13; s ^= s >> 7; s ^= s << 17;
-    h[i] = (int)(s % n);
-  }
-  CHECK(hipMemcpy(tab, h, n * sizeof(int), hipMemcpyHostToDevice));
-  printf("blocks  empty_us  chain1_us  chain2_us  chain4_us  chain8_us\n");
+  int* out;
+  CHECK(hipMalloc(&out, 4096 * sizeof(int)));
+  hipStream_t s;
+  CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  g_stream = s;
+
+  printf("# 1. dependent empty kernels, per launch (us)\n");
+  printf("blocks  eager  graph\n");
+  const int chain = 200;
   for (int blocks : {1, 64, 256, 1024, 4096}) {
-    float e = per_launch_us([&] { hipLaunchKernelGGL(k_empty, dim3(blocks), dim3(256), 0, 0, out); });
-    float c1 = per_launch_us([&] { hipLaunchKernelGGL(k_chain<1>, dim3(blocks), dim3(256), 0, 0, tab, out, n); });
-    float c2 = per_launch_us([&] { hipLaunchKernelGGL(k_chain<2>, dim3(blocks), dim3(256), 0, 0, tab, out, n); });
-    float c4 = per_launch_us([&] { hipLaunchKernelGGL(k_chain<4>, dim3(blocks), dim3(256), 0, 0, tab, out, n); });
-    float c8 = per_launch_us([&] { hipLaunchKernelGGL(k_chain<8>, dim3(blocks), dim3(256), 0, 0, tab, out, n); });
-    printf("%6d  %8.2f  %9.2f  %9.2f  %9.2f  %9.2f\n", blocks, e, c1, c2, c4, c8);
+    auto launch = [&] { hipLaunchKernelGGL(k_empty, dim3(blocks), dim3(256), 0, s, out); };
+    const float eager = time_us(launch, chain);
+    hipGraph_t g;
+    hipGraphExec_t ge;
+    CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    for (int i = 0; i < chain; ++i) launch();
+    CHECK(hipStreamEndCapture(s, &g));
+    CHECK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+    const float graph = time_us([&] { CHECK(hipGraphLaunch(ge, s)); }, 20) / chain;
+    printf("%6d  %5.2f  %5.2f\n", blocks, eager, graph);
+    CHECK(hipGraphExecDestroy(ge));
+    CHECK(hipGraphDestroy(g));
   }
+
+  int cus = 0;
+  CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+  unsigned *cnt, *fail;
+  CHECK(hipMalloc(&cnt, 64));
+  CHECK(hipMalloc(&fail, 64));
+  CHECK(hipMemset(fail, 0, 64));
+  auto reset = [&] { CHECK(hipMemsetAsync(cnt, 0, 64, s)); };
+
+  printf("# 2. grid barrier inside one launch (one chip counter), per barrier (us)\n");
+  printf("grid  per_barrier\n");
+  for (int grid : {cus / 4, cus, 2 * cus}) {
+    const int nbar = 200;
+    unsigned gen0 = 0;
+    reset();
+    const float t0 = time_us([&] {
+      hipLaunchKernelGGL(k_barriers, dim3(grid), dim3(256), 0, s, (gu32*)cnt, 0, (gu32*)fail,
+                         gen0);
+    }, 20);
+    const float t1 = time_us([&] {
+      hipLaunchKernelGGL(k_barriers, dim3(grid), dim3(256), 0, s, (gu32*)cnt, nbar,
+                         (gu32*)fail, gen0);
+      gen0 += nbar;
+    }, 20);
+    printf("%4d  %6.2f\n", grid, (t1 - t0) / nbar);
+  }
+
+  // ---- 3. PubMed-sized K-loop
+  const int n = 19717, m = 44324, f = 3, K = 10;
+  const float alpha = 0.1f;
+  std::vector<std::vector<int>> adj(n);
+  uint64_t st = 88172645463325252ull;
+  auto rnd = [&] {
+    st ^= st << 13; st ^= st >> 7; st ^= st << 17;
+    return st;
+  };
+  for (int e = 0; e < m; ++e) {
+    const int a = (int)(rnd() % n), b = (int)(rnd() % n);
+    if (a == b) continue;
+    adj[a].push_back(b);
+    adj[b].push_back(a);
+  }
+  std::vector<int> rp(n + 1, 0), cl;
+  std::vector<float> vl;
+  std::vector<double> deg(n);
+  for (int i = 0; i < n; ++i) {
+    adj[i].push_back(i);
+    std::sort(adj[i].begin(), adj[i].end());
+    adj[i].erase(std::unique(adj[i].begin(), adj[i].end()), adj[i].end());
+    deg[i] = (double)adj[i].size();
+  }
+  for (int i = 0; i < n; ++i) {
+    for (int j : adj[i]) {
+      cl.push_back(j);
+      vl.push_back((float)(1.0 / std::sqrt(deg[i]) / std::sqrt(deg[j])));
+    }
+    rp[i + 1] = (int)cl.size();
+  }
+  std::vector<float> hh((size_t)n * 4, 0.0f);
+  for (int i = 0; i < n; ++i)
+    for (int c = 0; c < f; ++c) hh[(size_t)i * 4 + c] = (float)((int)(rnd() % 2001) - 1000) / 1000.0f;
+  int *d_rp, *d_col;
+  float *d_val, *d_h, *z0, *z1, *w0, *w1;
+  CHECK(hipMalloc(&d_rp, rp.size() * 4));
+  CHECK(hipMalloc(&d_col, cl.size() * 4));
+  CHECK(hipMalloc(&d_val, vl.size() * 4));
+  CHECK(hipMalloc(&d_h, hh.size() * 4));
+  for (float** p : {&z0, &z1, &w0, &w1}) {
+    CHECK(hipMalloc(p, hh.size() * 4));
+    CHECK(hipMemset(*p, 0, hh.size() * 4));
+  }
+  CHECK(hipMemcpy(d_rp, rp.data(), rp.size() * 4, hipMemcpyHostToDevice));
+  CHECK(hipMemcpy(d_col, cl.data(), cl.size() * 4, hipMemcpyHostToDevice));
+  CHECK(hipMemcpy(d_val, vl.data(), vl.size() * 4, hipMemcpyHostToDevice));
+  CHECK(hipMemcpy(d_h, hh.data(), hh.size() * 4, hipMemcpyHostToDevice));
+  const int steps_grid = (n + 63) / 64;
+  // K dependent launches, captured
+  hipGraph_t g;
+  hipGraphExec_t ge;
+  CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+  const float* src = d_h;
+  for (int k = 0; k < K; ++k) {
+    float* dst = ((K - 1 - k) % 2 == 0) ? z0 : z1;
+    hipLaunchKernelGGL(k_step, dim3(steps_grid), dim3(256), 0, s, d_rp, d_col, d_val, src, d_h,
+                       dst, n, f, alpha);
+    src = dst;
+  }
+  CHECK(hipStreamEndCapture(s, &g));
+  CHECK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+  const float t_launches = time_us([&] { CHECK(hipGraphLaunch(ge, s)); }, 200);
+  printf("# 3. pubmed-sized APPNP, K = %d, F = %d, nnz = %zu\n", K, f, cl.size());
+  printf("variant                         grid  us_per_propagation  us_per_iteration\n");
+  printf("captured K launches            %5d  %18.2f  %16.2f\n", steps_grid, t_launches,
+         t_launches / K);
+  std::vector<float> ref(hh.size()), got(hh.size());
+  CHECK(hipMemcpy(ref.data(), z0, ref.size() * 4, hipMemcpyDeviceToHost));
+  for (int grid : {cus / 4, cus / 2, cus}) {
+    unsigned gen0 = 0;
+    reset();
+    auto run = [&] {
+      hipLaunchKernelGGL(k_loop, dim3(grid), dim3(256), 0, s, d_rp, d_col, d_val, d_h, w0, w1, n,
+                         f, alpha, K, (gu32*)cnt, (gu32*)fail, gen0);
+      gen0 += K - 1;
+    };
+    const float t = time_us(run, 200);
+    CHECK(hipMemcpy(got.data(), w0, got.size() * 4, hipMemcpyDeviceToHost));
+    const bool same = got == ref;
+    printf("persistent launch + barriers   %5d  %18.2f  %16.2f  %s\n", grid, t, t / K,
+           same ? "bitwise equal" : "MISMATCH");
+  }
+  unsigned hfail = 0;
+  CHECK(hipMemcpy(&hfail, fail, 4, hipMemcpyDeviceToHost));
+  printf("barrier spin give-ups: %u\n", hfail);
   return 0;
 }
