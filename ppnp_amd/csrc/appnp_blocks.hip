@@ -64,39 +64,8 @@ struct RemLayout {
   const uint32_t* ent;  // packed (row in group, column in block); padding: kRemNone
   const float* val;
   const int32_t* cblk;  // source block of each chunk of 64 entries
-  int32_t* done;        // pacing: [passes][kPaceGroups][nb] waves past each block, cumulative
-                        // over the call's iterations (zeroed per call); null: no pacing
   int32_t nb, br_log2, slots, rg, passes;
-  int32_t iter;         // index of this launch within the call
-  int32_t lead;         // blocks a wave may run ahead of its group's slowest wave
 };
-
-constexpr int kPaceGroups = 8;    // workgroups b, b+8, ... share an XCD (placement observed
-                                  // round-robin; speed only, never correctness)
-constexpr int kPaceSpins = 1024;  // bounded wait; a wave that runs out stops pacing
-
-// Lane 0 polls until ctr reaches target (relaxed agent-scope load: vector path, sc1).
-__device__ __forceinline__ bool pace_wait(int32_t* ctr, int target, int lane) {
-  int ok = 1;
-  if (lane == 0) {
-    __attribute__((address_space(1))) int32_t* c = (__attribute__((address_space(1))) int32_t*)ctr;
-    ok = 0;
-    for (int spin = 0; spin < kPaceSpins; ++spin) {
-      if (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) {
-        ok = 1;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
-  }
-  return __builtin_amdgcn_readfirstlane(ok) != 0;
-}
-
-__device__ __forceinline__ void pace_signal(int32_t* ctr, int lane) {
-  if (lane == 0)
-    __hip_atomic_fetch_add((__attribute__((address_space(1))) int32_t*)ctr, 1, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-}
 
 // ---- segmented inclusive scan over the 64 lanes (rows non-decreasing across lanes) --------
 // DPP (gfx9 family): row_shr:n shifts within each 16-lane row; row_bcast:15 / row_bcast:31
@@ -196,25 +165,11 @@ __global__ __launch_bounds__(kRemThreads) void k_rem_persist(StepArgs a, RemLayo
     const int64_t r0 = g * L.rg;
     const int rows = (int)max<int64_t>(0, min<int64_t>(L.rg, a.n_rows - r0));
     for (int r = lane; r < rows; r += kWave) acc[r] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    // pacing within this workgroup's XCD group: signal each block once this wave has passed
-    // it; before a round whose last block is b, wait for the group's waves to pass b - lead
-    const int grp = blockIdx.x % kPaceGroups;
-    const int target =
-        (L.iter + 1) * (((int)gridDim.x - grp + kPaceGroups - 1) / kPaceGroups) * kRemWaves;
-    int32_t* dn = L.done ? L.done + ((int64_t)p * kPaceGroups + grp) * L.nb : nullptr;
-    int sig = 0;  // next block to signal
-    bool pacing = dn != nullptr;
     // this wave's stream: blocks 0..nb-1 back to back, each a whole number of chunks; the
     // block of chunk c is cblk[c]
     const int32_t c_end = L.off[(g + 1) * L.nb] / kRemChunk;
     for (int32_t c = L.off[g * L.nb] / kRemChunk; c < c_end; c += U) {
       const int nch = min(U, c_end - c);
-      if (dn) {
-        const int b_first = L.cblk[c], b_last = L.cblk[c + nch - 1];
-        for (; sig < b_first; ++sig) pace_signal(dn + sig, lane);
-        if (pacing && b_last - L.lead >= 0)
-          pacing = pace_wait(dn + b_last - L.lead, target, lane);
-      }
       int64_t cbase[U];
 #pragma unroll
       for (int u = 0; u < U; ++u)
@@ -253,8 +208,6 @@ __global__ __launch_bounds__(kRemThreads) void k_rem_persist(StepArgs a, RemLayo
         }
       }
     }
-    if (dn)
-      for (; sig < L.nb; ++sig) pace_signal(dn + sig, lane);
     for (int r = lane; r < rows; r += kWave) rem_finish<EPI>(a, r0 + r, acc[r]);
   }
 }
@@ -476,24 +429,14 @@ int graph_build_source_blocks(appnp_graph* g, hipStream_t s) {
   return APPNP_OK;
 }
 
-// Pacing counters of one call (remainder pass): zeroed by the caller once per call.
-// APPNP_REM_LEAD (measurement): blocks a wave may lead its group by; 0 disables pacing.
-size_t remainder_counter_bytes(const appnp_graph* g) {
-  static const int lead = env_or("APPNP_REM_LEAD", 2);
-  if (!g->rb_off || lead <= 0) return 0;
-  return ((size_t)g->rb_passes * kPaceGroups * g->rb_nb * sizeof(int32_t) + 255) / 256 * 256;
-}
-
 // One iteration of the remainder columns: R = (M_k o A_hat) Z_rem over all source blocks in
 // one persistent launch (k_rem_persist), epilogue included.  a: the iteration's StepArgs
 // (dropout key, n_rows, scale, alpha); z_rem [n, 4]; h_rem = H + fs; out / ld_out / nv: where
 // the nv valid columns of Z_{k+1} go.  epi = EPI_BWD (adjoint): h_rem / ld_h are dH's
-// remainder columns, accumulated into; out (G_k's remainder) may be null.  done: the call's
-// pacing counters (remainder_counter_bytes; null: no pacing); iter: the launch's index within
-// the call.
+// remainder columns, accumulated into; out (G_k's remainder) may be null.
 hipError_t launch_remainder(const appnp_graph* g, const StepArgs& a_in, int epi,
                             const float* z_rem, const float* h_rem, int64_t ld_h, float* out,
-                            int64_t ld_out, int nv, int32_t* done, int iter, hipStream_t s) {
+                            int64_t ld_out, int nv, hipStream_t s) {
   StepArgs a = a_in;
   a.zin = z_rem;
   a.aux = nullptr;
@@ -509,10 +452,8 @@ hipError_t launch_remainder(const appnp_graph* g, const StepArgs& a_in, int epi,
   a.ld_out = ld_out;
   a.f = nv;
   if (a.n_rows <= 0) return hipSuccess;
-  static const int lead = env_or("APPNP_REM_LEAD", 2);
-  RemLayout L{g->rb_off, g->rb_ent,   g->rb_val,    g->rb_cblk, lead > 0 ? done : nullptr,
-              g->rb_nb,  g->rb_br_log2, g->rb_slots, g->rb_rg,  g->rb_passes,
-              iter,      lead};
+  RemLayout L{g->rb_off, g->rb_ent, g->rb_val, g->rb_cblk, g->rb_nb, g->rb_br_log2, g->rb_slots, g->rb_rg,
+              g->rb_passes};
   const size_t lds = (size_t)kRemWaves * g->rb_rg * sizeof(f32x4);
   const dim3 grid((unsigned)g->rb_grid), block(kRemThreads);
   if (epi == EPI_BWD) return launch_rem<EPI_BWD>(grid, block, lds, s, a, L);

@@ -137,21 +137,20 @@ int64_t split_point(const appnp_graph* g, int64_t f, int dtype, int V) {
 //   * main chain: K launches of the SpMM kernel on fs columns, gathering whole lines of the
 //     main parts (ping-pong between the two buffers, the last into Z[:, :fs]);
 //   * remainder chain: K persistent L2-resident passes over the remainder parts (the last
-//     into Z[:, fs:f]); their pacing counters (`done`, may be null) are zeroed once per call.
+//     into Z[:, fs:f]).
 // The chains touch disjoint parts of the buffers and disjoint columns of Z.  Both run on the
 // caller's stream: on a side stream they overlapped in time but shared the memory system, and
 // the total measured within 1 % of running them one after the other.
 int propagate_split(const appnp_graph* g, const StepArgs& a0, const void* H, int64_t ld_h,
                     void* Z, int64_t ld_z, int64_t fs, int K, float p_drop, uint64_t seed,
-                    char* ws, int64_t main_b, int64_t buf_b, int32_t* done, hipStream_t s) {
+                    char* ws, int64_t main_b, int64_t buf_b, hipStream_t s) {
   const int64_t n = a0.n_rows, f = a0.f;
   char* bufs[2] = {ws, ws + buf_b};
   auto main_of = [&](int i) { return reinterpret_cast<float*>(bufs[i]); };
   auto rem_of = [&](int i) { return reinterpret_cast<float*>(bufs[i] + main_b); };
   const float* h = static_cast<const float*>(H);
   float* z = static_cast<float*>(Z);
-  int rc = done ? dev_err(hipMemsetAsync(done, 0, appnp::remainder_counter_bytes(g), s)) : 0;
-  if (!rc) rc = dev_err(appnp::launch_split_copy(h, ld_h, n, f, fs, main_of(0), rem_of(0), s));
+  int rc = dev_err(appnp::launch_split_copy(h, ld_h, n, f, fs, main_of(0), rem_of(0), s));
   StepArgs am = a0, ar = a0;  // main / remainder chain
   am.f = (int32_t)fs;
   am.h = H;
@@ -170,7 +169,7 @@ int propagate_split(const appnp_graph* g, const StepArgs& a0, const void* H, int
     set_drop(ar, p_drop, seed, k);
     rc = dev_err(appnp::launch_remainder(g, ar, appnp::EPI_FWD, rem_of(cur), h + fs, ld_h,
                                          last ? z + fs : rem_of(dst), last ? ld_z : 4,
-                                         last ? (int)(f - fs) : 4, done, k, s));
+                                         last ? (int)(f - fs) : 4, s));
     cur = dst;
   }
   return rc;
@@ -181,16 +180,14 @@ int propagate_split(const appnp_graph* g, const StepArgs& a0, const void* H, int
 // self-adjoint A_hat.  dH = alpha dZ is set by the caller.
 int propagate_bwd_split(const appnp_graph* g, const StepArgs& a0, const void* dZ, int64_t ld_dz,
                         void* dH, int64_t ld_dh, int64_t fs, int K, float alpha, float p_drop,
-                        uint64_t seed, char* ws, int64_t main_b, int64_t buf_b, int32_t* done,
+                        uint64_t seed, char* ws, int64_t main_b, int64_t buf_b,
                         hipStream_t s) {
   const int64_t n = a0.n_rows, f = a0.f;
   char* bufs[2] = {ws, ws + buf_b};
   auto main_of = [&](int i) { return reinterpret_cast<float*>(bufs[i]); };
   auto rem_of = [&](int i) { return reinterpret_cast<float*>(bufs[i] + main_b); };
-  int rc = done ? dev_err(hipMemsetAsync(done, 0, appnp::remainder_counter_bytes(g), s)) : 0;
-  if (!rc)
-    rc = dev_err(appnp::launch_split_copy(static_cast<const float*>(dZ), ld_dz, n, f, fs,
-                                          main_of(0), rem_of(0), s));
+  int rc = dev_err(appnp::launch_split_copy(static_cast<const float*>(dZ), ld_dz, n, f, fs,
+                                            main_of(0), rem_of(0), s));
   StepArgs am = a0, ar = a0;  // main / remainder chain
   am.f = (int32_t)fs;
   am.aux = dH;
@@ -211,8 +208,7 @@ int propagate_bwd_split(const appnp_graph* g, const StepArgs& a0, const void* dZ
     set_drop(ar, p_drop, seed, k);
     ar.alpha = a_k;
     rc = dev_err(appnp::launch_remainder(g, ar, appnp::EPI_BWD, rem_of(cur), dh_rem, ld_dh,
-                                         k == 0 ? nullptr : rem_of(dst), 4, (int)(f - fs), done,
-                                         K - 1 - k, s));
+                                         k == 0 ? nullptr : rem_of(dst), 4, (int)(f - fs), s));
     cur = dst;
   }
   return rc;
@@ -335,8 +331,7 @@ size_t appnp_workspace_bytes(const appnp_graph* g, int64_t f, int64_t ld, int dt
   const int64_t rows = g->row_hi - g->row_lo;
   // two ping-pong buffers (the forward needs one -- two in the split layout, each as large
   // as a packed buffer -- the adjoint two), 256-B aligned each
-  return (size_t)(2 * rows * line_ld(f, dtype) * elem_size(dtype) + 2048) +
-         appnp::remainder_counter_bytes(g);
+  return (size_t)(2 * rows * line_ld(f, dtype) * elem_size(dtype) + 2048);
 }
 
 int appnp_graph_source_blocks(const appnp_graph* g, int64_t* bytes) {
@@ -386,17 +381,14 @@ int appnp_propagate(const appnp_graph* g, const void* H, int64_t ld_h, void* Z, 
   a.ld_h = ld_h;
   const int64_t fs = K >= 2 ? split_point(g, f, dtype, V) : 0;
   if (fs > 0) {
-    // the remainder pass's pacing counters, then two split buffers [n, fs] + [n, 4] fp32 in
-    // the workspace, each 256-B aligned
-    const size_t cb = appnp::remainder_counter_bytes(g);
+    // two split buffers [n, fs] + [n, 4] fp32 in the workspace, each 256-B aligned
     const int64_t main_b = (n * fs * 4 + 255) / 256 * 256;
     const int64_t buf_b = (main_b + n * 16 + 255) / 256 * 256;
     const size_t used = (size_t)(reinterpret_cast<uintptr_t>(ws) -
                                  reinterpret_cast<uintptr_t>(ws_orig));
-    if (ws_bytes >= used + cb + 2 * (size_t)buf_b)
+    if (ws_bytes >= used + 2 * (size_t)buf_b)
       return propagate_split(g, a, H, ld_h, Z, ld_z, fs, K, p_drop, seed,
-                             static_cast<char*>(ws) + cb, main_b, buf_b,
-                             cb ? static_cast<int32_t*>(ws) : nullptr, s);
+                             static_cast<char*>(ws), main_b, buf_b, s);
   }
   const void* src = H;
   int64_t ld_src = ld_h;
@@ -460,13 +452,12 @@ int appnp_propagate_bwd(const appnp_graph* g, const void* dZ, int64_t ld_dz, voi
   // split rows (self-adjoint A_hat: the source-blocked copy of A_hat is that of A_hat^T)
   const int64_t fs = (self_adjoint && K >= 2) ? split_point(g, f, dtype, V) : 0;
   int64_t main_b = 0, buf_b = 0;
-  const size_t cb = fs > 0 ? appnp::remainder_counter_bytes(g) : 0;
   if (fs > 0) {
     main_b = (n * fs * 4 + 255) / 256 * 256;
     buf_b = (main_b + n * 16 + 255) / 256 * 256;
     const size_t used = (size_t)(reinterpret_cast<uintptr_t>(ws) -
                                  reinterpret_cast<uintptr_t>(ws_orig));
-    if (ws_bytes < used + cb + 2 * (size_t)buf_b) main_b = 0;  // too small: whole rows
+    if (ws_bytes < used + 2 * (size_t)buf_b) main_b = 0;  // too small: whole rows
   }
   StepArgs a = base_args(g, f, alpha);
   if (!self_adjoint) {
@@ -481,8 +472,7 @@ int appnp_propagate_bwd(const appnp_graph* g, const void* dZ, int64_t ld_dz, voi
   a.tkey = 1;  // entry (j, i) of A_hat^T carries the mask of forward edge (i, j)
   if (fs > 0 && main_b > 0)
     return propagate_bwd_split(g, a, dZ, ld_dz, dH, ld_dh, fs, K, alpha, p_drop, seed,
-                               static_cast<char*>(ws) + cb, main_b, buf_b,
-                               cb ? static_cast<int32_t*>(ws) : nullptr, s);
+                               static_cast<char*>(ws), main_b, buf_b, s);
   a.aux = dH;
   a.ld_aux = ld_dh;
   const void* src = dZ;

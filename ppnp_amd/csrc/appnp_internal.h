@@ -77,10 +77,9 @@ hipError_t exclusive_scan(const int32_t* cnt, int64_t rows, int32_t* out, int64_
 
 // appnp_blocks.hip
 int graph_build_source_blocks(appnp_graph* g, hipStream_t s);
-size_t remainder_counter_bytes(const appnp_graph* g);
 hipError_t launch_remainder(const appnp_graph* g, const StepArgs& a, int epi,
                             const float* z_rem, const float* h_rem, int64_t ld_h, float* out,
-                            int64_t ld_out, int nv, int32_t* done, int iter, hipStream_t s);
+                            int64_t ld_out, int nv, hipStream_t s);
 hipError_t launch_split_copy(const float* h, int64_t ld_h, int64_t n, int64_t f, int64_t fs,
                              float* main, float* rem, hipStream_t s);
 
