@@ -13,9 +13,11 @@
 //     [b * 2^15, (b+1) * 2^15), i.e. 512 KB of Z_rem, which sits in every XCD's 4 MB L2 while
 //     the chip gathers from it.  Every wave walks the blocks in the same order at about the
 //     same rate, so the blocks live in L2 at one time are the few between the slowest and
-//     the fastest wave.  (Pacing the workgroups with per-block counters and a barrier kept
-//     that window at two blocks but drained each wave's pipeline at every block: 8.33 against
-//     8.15 ms per products-synth iteration without it.)
+//     the fastest wave.  Pacing measured slower every way it was tried: per-block counters
+//     with a workgroup barrier (8.33 against 8.15 ms per products-synth iteration), and
+//     per-wave signals with bounded waits inside groups of co-located workgroups, leading by
+//     1, 2 or 4 blocks (8.6 to 16.9 against 8.2 ms; tools/sweep_rem.sh, round-2 history).
+//     The gathers are close to the L2 request rate anyway: each is its own 16-B request.
 //
 // The accumulators never leave the chip.  The launch is persistent -- one 1024-thread
 // workgroup per CU, each of its 16 waves owning a group of <= 640 destination rows whose
