@@ -431,9 +431,9 @@ def main():
                 "ceiling_source": "tools/gather_probe.hip, profiles/r1_gather_probe.txt",
             },
             "kernel": ("k_step_wide (one launch per iteration)" if not fs else
-                       f"k_step_wide on columns [0, {fs}) of the slab + k_rem_block x "
-                       f"{-(-n // (1 << 17))} "
-                       f"(remainder columns, L2-blocked) per iteration; times are per iteration"),
+                       f"k_step_wide on columns [0, {fs}) of the slab + k_rem_persist (the "
+                       f"remainder columns, one persistent L2-blocked launch) per iteration; "
+                       f"times are per iteration"),
             "bytes_per_launch": b_iter,
             "avg_launch_ms": avg_launch_ms,
             # the access-pattern bound: every nonzero gathers a random row of Z,

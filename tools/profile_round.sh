@@ -20,6 +20,7 @@ tools/gpu_session.sh \
  "emu_r2c4ov::200::$B --layout 2x4 --overlap --emulate 8:0" \
  "emu_r4c2::200::$B --layout 4x2 --emulate 8:0" \
  "dc_col::200::$TR --nproc-per-node 2 tests/dist_worker.py --layout col" \
+ "dc_row_arxiv::300::$G --nproc-per-node 4 tests/dist_worker.py --layout row --overlap --workload arxiv-synth --oracle" \
  "dc_row::300::$G --nproc-per-node 2 tests/dist_worker.py --layout row" \
  "dc_row_ov::300::$G --nproc-per-node 2 tests/dist_worker.py --layout row --overlap --p-drop 0.3" \
  "dc_2x2::300::$G --nproc-per-node 4 tests/dist_worker.py --layout 2x2" \
@@ -31,4 +32,6 @@ tools/gpu_session.sh \
  "w_cora::200::$B --workload cora-ml" \
  "w_powerlaw::200::$B --workload products-powerlaw" \
  "w_local::200::$B --workload products-local" \
- "w_bf16::200::$B --dtype bf16"
+ "w_bf16::200::$B --dtype bf16" \
+ "dist2_auto::300::$G --nproc-per-node 2 bench.py --gpus 2 --steps 3 --warmup 1" \
+ "dist4_auto::300::$G --nproc-per-node 4 bench.py --gpus 4 --steps 3 --warmup 1"

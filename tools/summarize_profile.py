@@ -62,7 +62,7 @@ def main():
     p.add_argument("stats_dir")
     p.add_argument("fetch_dir")
     p.add_argument("write_dir")
-    p.add_argument("--kernels", default="k_step_,k_rem_block,k_split_copy",
+    p.add_argument("--kernels", default="k_step_,k_rem_persist,k_split_copy",
                    help="kernels of one iteration, the SpMM kernel (one per iteration) first")
     p.add_argument("--workload", default="products-synth")
     p.add_argument("--bench-json", default=None)
