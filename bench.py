@@ -162,6 +162,8 @@ def tune_layouts(cands, indptr, indices, n, H, K, alpha, dev, ctl_dev, reps=2):
 
     best, best_ms, times = None, None, {}
     for layout, overlap, exchange in cands:
+        if torch.distributed.get_rank() == 0:
+            log(f"[bench] autotune: building {layout} overlap={overlap} exchange={exchange}")
         r = pdist.PartitionedAPPNP.create(indptr, indices, n, H, K, alpha, dev, layout=layout,
                                           overlap=overlap, exchange=exchange)
         r.run()
@@ -177,6 +179,8 @@ def tune_layouts(cands, indptr, indices, n, H, K, alpha, dev, ctl_dev, reps=2):
         name = (f"rows{layout.rows}xcols{layout.cols}" + ("-overlap" if overlap else "")
                 + (f"-{exchange}" if layout.rows > 1 and layout.cols > 1 else ""))
         times[name] = ms
+        if torch.distributed.get_rank() == 0:
+            log(f"[bench] autotune {name}: {ms:.3f} ms per propagation")
         if best_ms is None or ms < best_ms:
             best, best_ms = r, ms
         else:
@@ -316,19 +320,22 @@ def main():
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
+    # one event per step boundary on the launch stream: the timed region's device time and the
+    # spread of the individual steps (reported as step_ms)
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    ev0, ev1 = evs[0], evs[-1]
     t0 = time.perf_counter()
     ev0.record(stream)
-    for _ in range(args.steps):
+    for i in range(args.steps):
         run()
-    ev1.record(stream)
+        evs[i + 1].record(stream)
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     dev_ms = ev0.elapsed_time(ev1)
+    steps_ms = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps))
     if world > 1:
         t = torch.tensor([wall, dev_ms], dtype=torch.float64, device=ctl_dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -393,6 +400,9 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": wall * 1e3 / args.steps,
+        # device time of each timed step on this rank (HIP events): spread of the run
+        "step_ms": {"min": steps_ms[0], "median": steps_ms[len(steps_ms) // 2],
+                    "max": steps_ms[-1]},
         "propagated_rows_per_s": rows_per_s,
         "higher_is_better": True,
         "scaling": "strong",

@@ -34,4 +34,4 @@ tools/gpu_session.sh \
  "w_local::200::$B --workload products-local" \
  "w_bf16::200::$B --dtype bf16" \
  "dist2_auto::300::$G --nproc-per-node 2 bench.py --gpus 2 --steps 3 --warmup 1" \
- "dist4_auto::300::$G --nproc-per-node 4 bench.py --gpus 4 --steps 3 --warmup 1"
+ "dist4_auto::300::$G --nproc-per-node 4 bench.py --gpus 4 --steps 3 --warmup 1 --workload arxiv-synth"
