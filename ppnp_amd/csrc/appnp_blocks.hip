@@ -353,7 +353,11 @@ int graph_build_source_blocks(appnp_graph* g, hipStream_t s) {
     return l;
   }();
   const int64_t nb = std::max<int64_t>(1, (g->n + (1LL << br_log2) - 1) >> br_log2);
-  if (nb > kWalkMaxBlocks) return APPNP_ENOTSUP;
+  // APPNP_SB_MAX_BLOCKS (tests): a lower block limit, read at every build, so a test can take
+  // the best-effort fallback on a small graph
+  const int max_blocks = std::min(kWalkMaxBlocks, std::max(1, env_or("APPNP_SB_MAX_BLOCKS",
+                                                                     kWalkMaxBlocks)));
+  if (nb > max_blocks) return APPNP_ENOTSUP;
   int dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||

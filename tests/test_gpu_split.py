@@ -234,3 +234,26 @@ def test_source_blocks_only_when_requested():
     assert ppnp_amd.Graph.from_scipy(a, device=DEV).source_block_bytes() == 0
     assert ppnp_amd.Graph.from_scipy(a, device=DEV, features=7).source_block_bytes() == 0
     assert ppnp_amd.Graph.from_scipy(a, device=DEV, features=100).source_block_bytes() > 0
+
+
+def test_source_blocks_best_effort_fallback(monkeypatch, ahat):
+    """a graph whose regrouped copy cannot be built (here: more source blocks than
+    the limit, lowered for the test) is still created, warns, and gathers whole rows --
+    with the same results."""
+    import ppnp_amd
+
+    monkeypatch.setenv("APPNP_SB_MAX_BLOCKS", "2")  # N = 300k needs 10 blocks of 2^15
+    with pytest.warns(RuntimeWarning, match="could not be built"):
+        G = ppnp_amd.Graph.from_csr(ahat.indptr, ahat.indices, None, N, device=DEV,
+                                    source_blocks=True)
+    assert G.source_block_bytes() == 0 and G.split_point(100) == 0
+    H = _h(100, 31)
+    Z = ppnp_amd.propagate_forward(G, H.to(DEV), 2, 0.1)
+    # ahat's pattern is A + I; an unweighted graph of that pattern (self loops merged) has the
+    # same A_hat up to the diagonal weight 2 -- compare against the oracle of that graph
+    import scipy.sparse as sp
+
+    a = sp.csr_matrix((np.ones(ahat.nnz, dtype=np.float32), ahat.indices, ahat.indptr),
+                      shape=ahat.shape)
+    close_fp32(Z.double().cpu().numpy(), O.appnp_propagate(O.calc_a_hat(a, "sym"), H.numpy(), 2,
+                                                           0.1))

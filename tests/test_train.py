@@ -47,19 +47,25 @@ def test_early_stopping_semantics():
 
 @pytest.mark.gpu
 def test_cora_accuracy_matches_run_sh():
-    """APPNP (K=10) trained with the main.py protocol reaches the reference's published
-    Cora-ML accuracy (run.sh:19-20: 0.856 +- 0.009 over 32 runs of PPNP)."""
-    s = T.main(["--dataset", "cora_ml", "--n-runs", "4", "--seed", "123"])
-    # the reference's own main.py re-run gives 0.830 +- 0.014 (SURVEY.md 3.1)
-    assert 0.81 <= s["valid_acc_mean"] <= 0.89, s
+    """APPNP (K=10) trained with the main.py protocol, 12 runs: the mean sits in the band of the
+    reference's published Cora-ML accuracy (run.sh:19-20: 0.856 +- 0.009 over 32 runs of PPNP;
+    the reference's own main.py re-run gives 0.830 +- 0.014), and within 0.015 of
+    the dense-PPR PPNP trained on the same 12 seeds and splits -- a paired check that catches a
+    regression of a point or two, where a run-to-run std of ~0.02 hides it in a 4-run band."""
+    s = T.main(["--dataset", "cora_ml", "--n-runs", "12", "--seed", "123"])
+    p = T.main(["--dataset", "cora_ml", "--n-runs", "12", "--seed", "123", "--model", "ppnp"])
+    assert 0.82 <= s["valid_acc_mean"] <= 0.87, s
+    assert s["valid_acc_std"] <= 0.035, s
+    assert abs(s["valid_acc_mean"] - p["valid_acc_mean"]) <= 0.015, (s, p)
 
 
 @pytest.mark.gpu
 def test_citeseer_accuracy_matches_run_sh():
     """run.sh:22-23 publishes Citeseer 0.760 +- 0.012 (PyTorch 1.2); the reference's main.py
-    re-run today gives 0.733 +- 0.014 (profiles/r1_train_accuracy.md)."""
-    s = T.main(["--dataset", "citeseer", "--n-runs", "4", "--seed", "123"])
-    assert 0.70 <= s["valid_acc_mean"] <= 0.79, s
+    re-run today gives 0.733 +- 0.014 (profiles/r1_train_accuracy.md).  12 runs."""
+    s = T.main(["--dataset", "citeseer", "--n-runs", "12", "--seed", "123"])
+    assert 0.71 <= s["valid_acc_mean"] <= 0.77, s
+    assert s["valid_acc_std"] <= 0.04, s
 
 
 @pytest.mark.gpu
