@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -123,6 +124,91 @@ __global__ __launch_bounds__(256) void k_loop(const int* rp, const int* col, con
     float* dst = ((K - 1 - k) % 2 == 0) ? z0 : z1;
     appnp_rows(rp, col, val, src, h, dst, n, f, alpha, blockIdx.x * 64, gridDim.x * 64);
     if (k + 1 < K) grid_barrier(cnt, gen0 + k + 1, fail);
+    src = dst;
+  }
+}
+
+// ---- 4. persistent K-loop shaped for latency: each workgroup keeps ITS rows' CSR in LDS
+// (iteration-invariant), every thread issues all the gathers of its rows before it sums them
+// (one dependent round per iteration instead of row_ptr -> col -> gather), and Z crosses
+// workgroups by write-through (sc1) stores and sc1 loads, so the barrier needs no fences:
+// every storing wave drains (vmcnt 0), the workgroup barrier, one agent-scope arrival, a
+// relaxed poll (MI355X_MICROARCH.md, valid forms, first row).
+constexpr int kSlots = 8;  // entries per row issued together; longer rows finish in a loop
+template <int J>           // rows per 4-lane group: 64 groups x J rows per block
+__global__ __launch_bounds__(256) void k_loop_lds(const int* rp, const int* col, const float* val,
+                                                  const float* h, float* z0, float* z1, int n,
+                                                  int f, float alpha, int K, gu32* cnt,
+                                                  gu32* fail, unsigned gen0) {
+  extern __shared__ int lds_i[];
+  constexpr int rows_per_block = 64 * J;
+  const int r0 = blockIdx.x * rows_per_block;
+  const int r1 = min(n, r0 + rows_per_block);
+  const int e0 = rp[r0], e1 = rp[r1];
+  int* lrp = lds_i;                                   // rows_per_block + 1
+  int* lcol = lds_i + rows_per_block + 1;             // entries of the block
+  float* lval = reinterpret_cast<float*>(lcol + (e1 - e0));
+  for (int i = threadIdx.x; i <= r1 - r0; i += 256) lrp[i] = rp[r0 + i] - e0;
+  for (int e = threadIdx.x; e < e1 - e0; e += 256) {
+    lcol[e] = col[e0 + e];
+    lval[e] = val[e0 + e];
+  }
+  __syncthreads();
+  const int sub = threadIdx.x >> 2, gl = threadIdx.x & 3;
+  const bool on = gl < f;
+  const float* src = h;
+  for (int k = 0; k < K; ++k) {
+    float* dst = ((K - 1 - k) % 2 == 0) ? z0 : z1;
+    float v[J][kSlots];
+    int b[J], e[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const int lr = sub + 64 * j;
+      const bool live = lr < r1 - r0 && on;
+      b[j] = live ? lrp[lr] : 0;
+      e[j] = live ? lrp[lr + 1] : 0;
+#pragma unroll
+      for (int t = 0; t < kSlots; ++t)
+        v[j][t] = b[j] + t < e[j]
+                      ? __hip_atomic_load(src + (int64_t)lcol[b[j] + t] * 4 + gl,
+                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                      : 0.0f;
+    }
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      float acc = 0.0f;
+#pragma unroll
+      for (int t = 0; t < kSlots; ++t)
+        if (b[j] + t < e[j]) acc = fmaf(lval[b[j] + t], v[j][t], acc);
+      for (int t = b[j] + kSlots; t < e[j]; ++t)
+        acc = fmaf(lval[t],
+                   __hip_atomic_load(src + (int64_t)lcol[t] * 4 + gl, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT),
+                   acc);
+      const int lr = sub + 64 * j;
+      if (lr < r1 - r0 && on) {
+        const int64_t o = (int64_t)(r0 + lr) * 4 + gl;
+        __hip_atomic_store(dst + o, fmaf(alpha, h[o], (1.0f - alpha) * acc), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    if (k + 1 < K) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned target = (gen0 + k + 1) * gridDim.x;
+        unsigned spins = 0;
+        while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+          __builtin_amdgcn_s_sleep(1);
+          if (++spins > (1u << 16)) {
+            __hip_atomic_store(fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+        }
+      }
+      __syncthreads();
+    }
     src = dst;
   }
 }
@@ -261,6 +347,36 @@ int main() {
     printf("persistent launch + barriers   %5d  %18.2f  %16.2f  %s\n", grid, t, t / K,
            same ? "bitwise equal" : "MISMATCH");
   }
+  // variant 4: CSR in LDS, all gathers of a thread's rows in flight, write-through hand-off
+  auto variant4 = [&](auto kern, int J) {
+    const int rows_per_block = 64 * J;
+    const int grid4 = (n + rows_per_block - 1) / rows_per_block;
+    int max_e = 0;
+    for (int b = 0; b < grid4; ++b) {
+      const int lo = b * rows_per_block, hi = std::min(n, lo + rows_per_block);
+      max_e = std::max(max_e, rp[hi] - rp[lo]);
+    }
+    const size_t lds4 = (size_t)(rows_per_block + 1 + 2 * max_e) * 4;
+    unsigned gen0 = 0;
+    reset();
+    CHECK(hipMemset(w0, 0, hh.size() * 4));
+    auto run = [&] {
+      hipLaunchKernelGGL(kern, dim3(grid4), dim3(256), lds4, s, d_rp, d_col, d_val, d_h, w0, w1,
+                         n, f, alpha, K, (gu32*)cnt, (gu32*)fail, gen0);
+      gen0 += K - 1;
+    };
+    const float t = time_us(run, 200);
+    CHECK(hipMemcpy(got.data(), w0, got.size() * 4, hipMemcpyDeviceToHost));
+    double err = 0.0;
+    for (size_t i = 0; i < got.size(); ++i)
+      err = std::max(err, (double)std::fabs(got[i] - ref[i]));
+    printf("LDS CSR + sc1, %d rows/group   %5d  %18.2f  %16.2f  max|diff| %.2e (LDS %zu B)\n", J,
+           grid4, t, t / K, err, lds4);
+  };
+  variant4(k_loop_lds<1>, 1);
+  variant4(k_loop_lds<2>, 2);
+  variant4(k_loop_lds<4>, 4);
+  variant4(k_loop_lds<8>, 8);
   unsigned hfail = 0;
   CHECK(hipMemcpy(&hfail, fail, 4, hipMemcpyDeviceToHost));
   printf("barrier spin give-ups: %u\n", hfail);
