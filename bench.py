@@ -154,30 +154,51 @@ def cpu_baseline(graph, H, K, alpha, iters, adj=None):
     return res, Zc
 
 
-def tune_layouts(cands, indptr, indices, n, H, K, alpha, dev, ctl_dev, reps=2):
+def tune_layouts(cands, indptr, indices, n, H, K, alpha, dev, ctl, reps=2):
     """Build each candidate layout, time ``reps`` propagations after one warm-up (barrier on
     both sides, max over ranks: every rank sees the same numbers and picks the same layout),
-    keep the fastest and free the others."""
+    keep the fastest and free the others.  A candidate that raises on any rank (agreed over the
+    gloo control group ``ctl``, which an RCCL error cannot poison) is recorded as failed and
+    skipped, so one broken exchange does not cost the whole scaling run."""
     from ppnp_amd import dist as pdist
 
     best, best_ms, times = None, None, {}
     for layout, overlap, exchange in cands:
-        if torch.distributed.get_rank() == 0:
-            log(f"[bench] autotune: building {layout} overlap={overlap} exchange={exchange}")
-        r = pdist.PartitionedAPPNP.create(indptr, indices, n, H, K, alpha, dev, layout=layout,
-                                          overlap=overlap, exchange=exchange)
-        r.run()
-        torch.cuda.synchronize()
-        torch.distributed.barrier()
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            r.run()
-        torch.cuda.synchronize()
-        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=ctl_dev)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        ms = float(t.item()) * 1e3 / reps
         name = (f"rows{layout.rows}xcols{layout.cols}" + ("-overlap" if overlap else "")
                 + (f"-{exchange}" if layout.rows > 1 and layout.cols > 1 else ""))
+        if torch.distributed.get_rank() == 0:
+            log(f"[bench] autotune: building {layout} overlap={overlap} exchange={exchange}")
+        r, err, dt = None, "", 0.0
+        try:
+            r = pdist.PartitionedAPPNP.create(indptr, indices, n, H, K, alpha, dev,
+                                              layout=layout, overlap=overlap, exchange=exchange)
+            r.run()
+            torch.cuda.synchronize()
+        except Exception as e:  # noqa: BLE001 -- reported and agreed on below
+            err = f"{type(e).__name__}: {e}"
+        failed = torch.tensor([1.0 if err else 0.0], dtype=torch.float64)
+        torch.distributed.all_reduce(failed, op=torch.distributed.ReduceOp.MAX, group=ctl)
+        if float(failed) == 0.0:
+            torch.distributed.barrier(group=ctl)
+            t0 = time.perf_counter()
+            try:
+                for _ in range(reps):
+                    r.run()
+                torch.cuda.synchronize()
+                dt = time.perf_counter() - t0
+            except Exception as e:  # noqa: BLE001
+                err = f"{type(e).__name__}: {e}"
+            t = torch.tensor([dt, 1.0 if err else 0.0], dtype=torch.float64)
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX, group=ctl)
+            dt, failed = float(t[0]), t[1:]
+        if float(failed) != 0.0:
+            times[name] = None
+            log(f"[bench] autotune {name}: FAILED on rank {torch.distributed.get_rank()}"
+                + (f": {err}" if err else " (another rank failed)"))
+            del r
+            torch.cuda.empty_cache()
+            continue
+        ms = dt * 1e3 / reps
         times[name] = ms
         if torch.distributed.get_rank() == 0:
             log(f"[bench] autotune {name}: {ms:.3f} ms per propagation")
@@ -186,6 +207,8 @@ def tune_layouts(cands, indptr, indices, n, H, K, alpha, dev, ctl_dev, reps=2):
         else:
             del r
         torch.cuda.empty_cache()
+    if best is None:
+        raise RuntimeError(f"every candidate layout failed: {times}")
     return best, times
 
 
@@ -240,7 +263,11 @@ def main():
                                                  timeout=datetime.timedelta(minutes=5))
         else:
             torch.distributed.init_process_group(backend)
-    ctl_dev = dev if world > 1 and torch.distributed.get_backend() == "nccl" else "cpu"
+    # control plane (barriers, max over ranks, failure agreement) on gloo over host memory:
+    # RCCL carries only the data-path exchange
+    ctl = None
+    if world > 1 and torch.distributed.get_backend() == "nccl":
+        ctl = torch.distributed.new_group(backend="gloo")
 
     t0 = time.perf_counter()
     indptr, indices = synth.graph_for(args.workload, device=dev)
@@ -262,7 +289,7 @@ def main():
                                                    layout=layout, overlap=overlap,
                                                    exchange=exchange, **emu)
         else:
-            runner, autotune = tune_layouts(cands, indptr, indices, n, H, K, alpha, dev, ctl_dev)
+            runner, autotune = tune_layouts(cands, indptr, indices, n, H, K, alpha, dev, ctl)
         torch.cuda.synchronize()
         t_build = time.perf_counter() - t1
         graph = runner.graph
@@ -270,9 +297,9 @@ def main():
         stream = torch.cuda.current_stream(dev)
         F_local = runner.width
         mine = graph.nnz_hat if runner.layout.coords(runner.rank)[1] == 0 else 0
-        nnz_t = torch.tensor([mine], dtype=torch.int64, device=ctl_dev)
+        nnz_t = torch.tensor([mine], dtype=torch.int64)
         if world > 1:
-            torch.distributed.all_reduce(nnz_t)
+            torch.distributed.all_reduce(nnz_t, group=ctl)
         nnz_total = int(nnz_t.item())
     else:
         t1 = time.perf_counter()
@@ -318,7 +345,7 @@ def main():
         run()
     torch.cuda.synchronize()
     if world > 1:
-        torch.distributed.barrier()
+        torch.distributed.barrier(group=ctl)
     torch.cuda.synchronize()
     # one event per step boundary on the launch stream: the timed region's device time and the
     # spread of the individual steps (reported as step_ms)
@@ -331,14 +358,14 @@ def main():
         evs[i + 1].record(stream)
     torch.cuda.synchronize()
     if world > 1:
-        torch.distributed.barrier()
+        torch.distributed.barrier(group=ctl)
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     dev_ms = ev0.elapsed_time(ev1)
     steps_ms = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps))
     if world > 1:
-        t = torch.tensor([wall, dev_ms], dtype=torch.float64, device=ctl_dev)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        t = torch.tensor([wall, dev_ms], dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX, group=ctl)
         wall, dev_ms = float(t[0]), float(t[1])
 
     # parity of the timed result: at N > 1 every rank compares its block of Z_K with a
@@ -353,9 +380,9 @@ def main():
         blk = Zref[runner.lo:runner.hi, runner.f_lo:runner.f_hi]
         err = float((Zblk.double() - blk.double()).abs().max()) if blk.numel() else 0.0
         ref_max = float(Zref.abs().max())
-        e = torch.tensor([err, ref_max], dtype=torch.float64, device=ctl_dev)
+        e = torch.tensor([err, ref_max], dtype=torch.float64)
         if world > 1:
-            torch.distributed.all_reduce(e, op=torch.distributed.ReduceOp.MAX)
+            torch.distributed.all_reduce(e, op=torch.distributed.ReduceOp.MAX, group=ctl)
         err, ref_max = float(e[0]), float(e[1])
         tol = 1e-5 * ref_max + 1e-6
         dist_parity = {"max_abs_err": err, "tol": tol, "max_abs_ref": ref_max,

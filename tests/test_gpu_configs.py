@@ -149,3 +149,24 @@ def test_stream_done_orders_consumer_after_side_stream():
     y = x * 2.0  # on the main stream
     assert bool((y == 2.0).all())
     _StreamDone(None).wait()  # a synchronous exchange hands over no event
+
+
+def test_bench_two_ranks_autotune_and_parity():
+    """The driver's N = 2 bench shape, rehearsed on the one GPU: bench.py under
+    torch.distributed.run (fresh child processes, gloo exchange since both ranks share the
+    device) times every candidate layout, keeps the fastest and checks its Z_K against a
+    single-GPU propagation of the whole graph (the line's parity field)."""
+    import json
+
+    env = dict(os.environ, PPNP_DIST_BACKEND="gloo", PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--workload", "arxiv-synth",
+           "--steps", "2", "--warmup", "1"]
+    proc = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=150)
+    assert proc.returncode == 0, proc.stdout[-3000:] + proc.stderr[-3000:]
+    res = json.loads([l for l in proc.stdout.splitlines() if l.startswith("{")][-1])
+    assert res["n_gpus"] == 2 and res["value"] > 0
+    assert res["parity"]["ok"], res["parity"]
+    tried = res["config"]["autotune_ms_per_step"]
+    assert len(tried) >= 2 and all(v is not None for v in tried.values()), tried
