@@ -229,6 +229,64 @@ int appnp_plan_create(const appnp_graph* g, const void* H, int64_t ld_h, void* Z
 int appnp_plan_launch(const appnp_plan* p, void* stream);
 void appnp_plan_destroy(appnp_plan* p);
 
+/*
+ * Row-partitioned multi-GPU propagation: SURVEY.md 8(b)'s appnp_dist_create, the loop of
+ * ppnp_amd/dist.py PartitionedAPPNP.run for a pure row layout, and the replacement of the
+ * reference's single-device product model.py:63 for graphs that outgrow one GPU.
+ *
+ * Rank r of P holds rows [r S, min(n, (r+1) S)) of A_hat, S = ceil(n / P).  After every
+ * iteration but the last, the ranks exchange their new row shards through a caller-supplied
+ * all-gather, so the library owns no communicator.  With overlap, each iteration first
+ * applies the local-column part of the rows on `stream`, while the previous exchange still
+ * runs on an internal stream, then waits for it and finishes with the remote columns.
+ */
+typedef struct appnp_dist appnp_dist;
+
+/*
+ * In-place all-gather of equal row shards.  `buf` is a device buffer of nranks * shard_bytes;
+ * this rank's shard sits at rank * shard_bytes and is complete in stream order on `stream`.
+ * The function must leave every rank's shard in place in stream order on `stream`. It can
+ * enqueue the exchange there, as ncclAllGather(buf + rank * shard_bytes, buf, shard_bytes,
+ * ncclChar, comm, stream) does (appnp_allgather_rccl). Or it can synchronise `stream`, exchange
+ * and return.  It returns 0 or a negative code, which appnp_dist_propagate passes on.
+ */
+typedef int (*appnp_allgather_fn)(void* buf, size_t shard_bytes, int rank, int nranks,
+                                  void* stream, void* ctx);
+
+/* indptr/indices/vals/n/nnz/mode: the WHOLE graph's A on this device, as appnp_graph_create.
+ * overlap != 0 keeps the held rows as local- and remote-column CSRs (fp32 propagation only).
+ * allgather/ctx: the exchange, called once per exchanged iterate by every rank. */
+int appnp_dist_create(const int32_t* indptr, const int32_t* indices, const float* vals,
+                      int64_t n, int64_t nnz, int mode, int rank, int nranks, int overlap,
+                      appnp_allgather_fn allgather, void* ctx, void* stream, appnp_dist** out);
+
+/* The held rows [row_lo, row_hi), the shard height S, and the graph of those rows. */
+int appnp_dist_rows(const appnp_dist* d, int64_t* row_lo, int64_t* row_hi, int64_t* shard);
+const appnp_graph* appnp_dist_graph(const appnp_dist* d);
+
+/* Workspace of appnp_dist_propagate: two full-height iterates (P S rows, line-aligned) and, with
+ * overlap, the fp32 local-column partial of the held rows. */
+size_t appnp_dist_workspace_bytes(const appnp_dist* d, int64_t f, int dtype);
+
+/*
+ * Z = the held rows of APPNP_K(H), given the held rows of H (row_hi - row_lo rows each;
+ * leading dimensions ld_h, ld_z; same semantics, dropout hash and results as appnp_propagate
+ * on the whole graph).  Collective: every rank calls it with the same f, dtype, K, alpha,
+ * p_drop and seed.  Stream-ordered on `stream`; no allocation; the exchange callback runs on
+ * the calling thread.
+ */
+int appnp_dist_propagate(appnp_dist* d, const void* H, int64_t ld_h, void* Z, int64_t ld_z,
+                         int64_t f, int dtype, int K, float alpha, float p_drop, uint64_t seed,
+                         void* ws, size_t ws_bytes, void* stream);
+void appnp_dist_destroy(appnp_dist* d);
+
+/* appnp_allgather_fn over RCCL; ctx is the ncclComm_t of the P ranks, rank order = row order.
+ * RCCL is resolved at first use (the librccl.so.1 already loaded in the process, e.g.
+ * PyTorch's, else the system one; APPNP_RCCL_LIB overrides), so the library does not link it.
+ * APPNP_ENOTSUP if it cannot be loaded, APPNP_EDEVICE if the call fails. */
+int appnp_allgather_rccl(void* buf, size_t shard_bytes, int rank, int nranks, void* stream,
+                         void* ctx);
+
 #ifdef __cplusplus
 }
 #endif

@@ -76,6 +76,19 @@ _SIGS = {
     ),
     "appnp_plan_launch": (_i32, [_vp, _vp]),
     "appnp_plan_destroy": (None, [_vp]),
+    "appnp_dist_create": (
+        _i32,
+        [_vp, _vp, _vp, _i64, _i64, _i32, _i32, _i32, _i32, _vp, _vp, _vp, C.POINTER(_vp)],
+    ),
+    "appnp_dist_rows": (_i32, [_vp, C.POINTER(_i64), C.POINTER(_i64), C.POINTER(_i64)]),
+    "appnp_dist_graph": (_vp, [_vp]),
+    "appnp_dist_workspace_bytes": (_sz, [_vp, _i64, _i32]),
+    "appnp_dist_propagate": (
+        _i32,
+        [_vp, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _f32, _f32, _u64, _vp, _sz, _vp],
+    ),
+    "appnp_dist_destroy": (None, [_vp]),
+    "appnp_allgather_rccl": (_i32, [_vp, _sz, _i32, _i32, _vp, _vp]),
     "appnp_step": (
         _i32,
         [_vp, _i32, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _f32,
@@ -84,6 +97,9 @@ _SIGS = {
 }
 
 EXPORTED = tuple(_SIGS)
+
+# appnp_allgather_fn (include/ppnp_amd.h): in-place all-gather of equal row shards
+ALLGATHER_FN = C.CFUNCTYPE(_i32, _vp, _sz, _i32, _i32, _vp, _vp)
 
 _lib = None
 

@@ -1,0 +1,238 @@
+// appnp_dist.hip -- row-partitioned multi-GPU propagation behind the C ABI
+// (include/ppnp_amd.h appnp_dist_*; SURVEY.md 8(b) "appnp_dist_create").
+//
+// Host orchestration only: every iteration is one or two appnp_step launches on the held rows
+// (appnp_capi.hip), and the row shards travel through the caller's all-gather callback.  The
+// schedule is ppnp_amd/dist.py PartitionedAPPNP.run for a pure row layout:
+//
+//   Z_0: H's held rows -> buffer 0 at [lo, hi), all-gather (every rank needs all of Z_0)
+//   k = 0 .. K-1:  src = buffer k&1 (all P S rows), dst = buffer (k+1)&1 at [lo, hi)
+//                  -- or Z itself on the last iteration (no exchange follows it)
+//     overlap:     LOCAL  (columns in [lo, hi): own shard, complete)  -> fp32 partial
+//                  wait for the exchange of src (internal stream)
+//                  REMOTE (the other columns) + partial + alpha H      -> dst
+//     otherwise:   ALL                                                -> dst
+//     k < K-1:     exchange dst (overlap: on the internal stream, behind an event on `stream`;
+//                  waited for inside the next iteration)
+//
+// The two buffers alternate, and each exchange is waited for before its buffer is written
+// again.  So the only concurrent accesses are the exchange of src, which writes the other
+// ranks' shards, and the local-column step, which reads this rank's shard.
+#include <dlfcn.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <new>
+
+#include "../../include/ppnp_amd.h"
+#include "appnp_internal.h"
+
+struct appnp_dist {
+  appnp_graph* g = nullptr;
+  int64_t n = 0, lo = 0, hi = 0, shard = 0;
+  int rank = 0, nranks = 1, overlap = 0;
+  appnp_allgather_fn allgather = nullptr;
+  void* ctx = nullptr;
+  hipStream_t xs = nullptr;            // exchange stream (overlap)
+  hipEvent_t produced = nullptr;       // dst rows written on the caller's stream
+  hipEvent_t exchanged = nullptr;      // exchange finished on xs
+};
+
+namespace {
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+inline int dev_err(hipError_t e) {
+  if (e == hipSuccess) return APPNP_OK;
+  if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) return APPNP_ENOMEM;
+  if (e == hipErrorInvalidValue) return APPNP_EINVAL;
+  return APPNP_EDEVICE;
+}
+
+constexpr size_t kAlign = 256;
+
+inline size_t align_up(size_t x) { return (x + kAlign - 1) / kAlign * kAlign; }
+
+struct WsLayout {
+  int64_t ld = 0;          // elements per row of the iterate buffers
+  size_t buf_bytes = 0;    // one full-height iterate
+  size_t partial_off = 0;  // fp32 partial (overlap)
+  size_t total = 0;
+};
+
+WsLayout ws_layout(const appnp_dist* d, int64_t f, int dtype) {
+  WsLayout w;
+  const int64_t es = dtype == APPNP_F32 ? 4 : 2;
+  w.ld = appnp::line_ld(f, dtype);
+  w.buf_bytes = align_up((size_t)(d->shard * d->nranks) * (size_t)(w.ld * es));
+  w.partial_off = 2 * w.buf_bytes;
+  const size_t partial = d->overlap ? align_up((size_t)d->shard * (size_t)w.ld * 4) : 0;
+  w.total = w.partial_off + partial;
+  return w;
+}
+
+// rows x (f elements) between two row-major matrices with leading dimensions in elements
+hipError_t copy_rows(void* dst, int64_t ld_dst, const void* src, int64_t ld_src, int64_t rows,
+                     int64_t f, int64_t es, hipStream_t s) {
+  if (rows <= 0 || f <= 0) return hipSuccess;
+  return hipMemcpy2DAsync(dst, (size_t)(ld_dst * es), src, (size_t)(ld_src * es),
+                          (size_t)(f * es), (size_t)rows, hipMemcpyDeviceToDevice, s);
+}
+
+// RCCL, resolved at first use (appnp_allgather_rccl)
+typedef int (*nccl_allgather_t)(const void*, void*, size_t, int, void*, hipStream_t);
+
+nccl_allgather_t rccl_allgather() {
+  static nccl_allgather_t fn = [] {
+    const char* env = std::getenv("APPNP_RCCL_LIB");
+    void* h = nullptr;
+    if (env && *env) {
+      h = dlopen(env, RTLD_NOW | RTLD_LOCAL);
+    } else {
+      // the copy already in the process (PyTorch's), so its communicators are valid here
+      h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+      if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    }
+    return h ? reinterpret_cast<nccl_allgather_t>(dlsym(h, "ncclAllGather")) : nullptr;
+  }();
+  return fn;
+}
+
+}  // namespace
+
+extern "C" {
+
+int appnp_dist_create(const int32_t* indptr, const int32_t* indices, const float* vals,
+                      int64_t n, int64_t nnz, int mode, int rank, int nranks, int overlap,
+                      appnp_allgather_fn allgather, void* ctx, void* stream, appnp_dist** out) {
+  if (!out) return APPNP_EINVAL;
+  *out = nullptr;
+  if (n <= 0 || nranks < 1 || rank < 0 || rank >= nranks || (nranks > 1 && !allgather))
+    return APPNP_EINVAL;
+  appnp_dist* d = new (std::nothrow) appnp_dist();
+  if (!d) return APPNP_ENOMEM;
+  d->n = n;
+  d->rank = rank;
+  d->nranks = nranks;
+  d->overlap = (overlap && nranks > 1) ? 1 : 0;
+  d->allgather = allgather;
+  d->ctx = ctx;
+  d->shard = (n + nranks - 1) / nranks;
+  d->lo = std::min<int64_t>(n, (int64_t)rank * d->shard);
+  d->hi = std::min<int64_t>(n, d->lo + d->shard);
+  int rc = appnp_graph_create_rows(indptr, indices, vals, n, nnz, mode, d->lo, d->hi,
+                                   d->overlap, stream, &d->g);
+  if (rc == APPNP_OK && d->overlap) {
+    rc = dev_err(hipStreamCreateWithFlags(&d->xs, hipStreamNonBlocking));
+    if (rc == APPNP_OK) rc = dev_err(hipEventCreateWithFlags(&d->produced, hipEventDisableTiming));
+    if (rc == APPNP_OK)
+      rc = dev_err(hipEventCreateWithFlags(&d->exchanged, hipEventDisableTiming));
+  }
+  if (rc != APPNP_OK) {
+    appnp_dist_destroy(d);
+    return rc;
+  }
+  *out = d;
+  return APPNP_OK;
+}
+
+int appnp_dist_rows(const appnp_dist* d, int64_t* row_lo, int64_t* row_hi, int64_t* shard) {
+  if (!d) return APPNP_EINVAL;
+  if (row_lo) *row_lo = d->lo;
+  if (row_hi) *row_hi = d->hi;
+  if (shard) *shard = d->shard;
+  return APPNP_OK;
+}
+
+const appnp_graph* appnp_dist_graph(const appnp_dist* d) { return d ? d->g : nullptr; }
+
+size_t appnp_dist_workspace_bytes(const appnp_dist* d, int64_t f, int dtype) {
+  if (!d || f <= 0 || (dtype != APPNP_F32 && dtype != APPNP_BF16)) return 0;
+  return ws_layout(d, f, dtype).total;
+}
+
+int appnp_dist_propagate(appnp_dist* d, const void* H, int64_t ld_h, void* Z, int64_t ld_z,
+                         int64_t f, int dtype, int K, float alpha, float p_drop, uint64_t seed,
+                         void* ws, size_t ws_bytes, void* stream) {
+  if (!d || f < 0 || K < 0 || (dtype != APPNP_F32 && dtype != APPNP_BF16)) return APPNP_EINVAL;
+  if (d->overlap && dtype != APPNP_F32) return APPNP_ENOTSUP;
+  if (!(alpha >= 0.0f && alpha <= 1.0f) || !(p_drop >= 0.0f && p_drop < 1.0f))
+    return APPNP_EINVAL;
+  const int64_t rows = d->hi - d->lo;
+  if (f == 0) return APPNP_OK;
+  if (rows > 0 && (!H || !Z || ld_h < f || ld_z < f)) return APPNP_EINVAL;
+  const int64_t es = dtype == APPNP_F32 ? 4 : 2;
+  hipStream_t s = as_stream(stream);
+  if (K == 0) return dev_err(copy_rows(Z, ld_z, H, ld_h, rows, f, es, s));
+  const WsLayout w = ws_layout(d, f, dtype);
+  if (!ws || ws_bytes < w.total) return APPNP_EINVAL;
+  char* base = static_cast<char*>(ws);
+  char* buf[2] = {base, base + w.buf_bytes};
+  float* partial = d->overlap ? reinterpret_cast<float*>(base + w.partial_off) : nullptr;
+  const size_t row_bytes = (size_t)(w.ld * es);
+  const size_t shard_bytes = (size_t)d->shard * row_bytes;
+  auto own = [&](char* b) { return b + (size_t)d->lo * row_bytes; };
+
+  // Z_0: the held rows of H, then the whole of it by exchange (synchronous in stream order)
+  int rc = dev_err(copy_rows(own(buf[0]), w.ld, H, ld_h, rows, f, es, s));
+  if (rc == APPNP_OK && d->nranks > 1)
+    rc = d->allgather(buf[0], shard_bytes, d->rank, d->nranks, s, d->ctx);
+  bool pending = false;  // an exchange on xs not yet waited for by `s`
+  for (int k = 0; k < K && rc == APPNP_OK; ++k) {
+    const bool last = k == K - 1;
+    char* src = buf[k & 1];
+    void* dst = last ? Z : static_cast<void*>(own(buf[(k + 1) & 1]));
+    const int64_t ld_dst = last ? ld_z : w.ld;
+    if (d->overlap) {
+      rc = appnp_step(d->g, APPNP_PART_LOCAL, src, w.ld, nullptr, 0, partial, w.ld, nullptr, 0,
+                      f, dtype, k, alpha, p_drop, seed, s);
+      if (rc == APPNP_OK && pending) {
+        rc = dev_err(hipStreamWaitEvent(s, d->exchanged, 0));
+        pending = false;
+      }
+      if (rc == APPNP_OK)
+        rc = appnp_step(d->g, APPNP_PART_REMOTE, src, w.ld, H, ld_h, dst, ld_dst, partial, w.ld,
+                        f, dtype, k, alpha, p_drop, seed, s);
+    } else {
+      rc = appnp_step(d->g, APPNP_PART_ALL, src, w.ld, H, ld_h, dst, ld_dst, nullptr, 0, f,
+                      dtype, k, alpha, p_drop, seed, s);
+    }
+    if (rc != APPNP_OK || last || d->nranks == 1) continue;
+    char* next = buf[(k + 1) & 1];
+    if (d->overlap) {
+      rc = dev_err(hipEventRecord(d->produced, s));
+      if (rc == APPNP_OK) rc = dev_err(hipStreamWaitEvent(d->xs, d->produced, 0));
+      if (rc == APPNP_OK) rc = d->allgather(next, shard_bytes, d->rank, d->nranks, d->xs, d->ctx);
+      if (rc == APPNP_OK) rc = dev_err(hipEventRecord(d->exchanged, d->xs));
+      pending = rc == APPNP_OK;
+    } else {
+      rc = d->allgather(next, shard_bytes, d->rank, d->nranks, s, d->ctx);
+    }
+  }
+  if (pending) (void)hipStreamWaitEvent(s, d->exchanged, 0);  // never leave xs running ahead
+  return rc;
+}
+
+void appnp_dist_destroy(appnp_dist* d) {
+  if (!d) return;
+  if (d->xs) (void)hipStreamSynchronize(d->xs);
+  if (d->produced) (void)hipEventDestroy(d->produced);
+  if (d->exchanged) (void)hipEventDestroy(d->exchanged);
+  if (d->xs) (void)hipStreamDestroy(d->xs);
+  appnp_graph_destroy(d->g);
+  delete d;
+}
+
+int appnp_allgather_rccl(void* buf, size_t shard_bytes, int rank, int nranks, void* stream,
+                         void* ctx) {
+  if (!buf || !ctx || rank < 0 || rank >= nranks) return APPNP_EINVAL;
+  const nccl_allgather_t fn = rccl_allgather();
+  if (!fn) return APPNP_ENOTSUP;
+  char* b = static_cast<char*>(buf);
+  // ncclChar = 0; ncclSuccess = 0
+  return fn(b + (size_t)rank * shard_bytes, b, shard_bytes, 0, ctx, as_stream(stream)) == 0
+             ? APPNP_OK
+             : APPNP_EDEVICE;
+}
+
+}  // extern "C"

@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include "appnp_device.h"
+#include "../../include/ppnp_amd.h"
 
 struct appnp_graph {
   int64_t n = 0;         // global node count
@@ -89,5 +90,40 @@ int pick_vec(int dtype, int64_t f, const int64_t* lds, int n_ld, const void* con
 hipError_t launch_step(int dtype, int epi, int V, const StepArgs& a, hipStream_t s);
 hipError_t launch_scale_rows(int dtype, const void* src, int64_t ld_src, void* dst,
                              int64_t ld_dst, int64_t n, int64_t f, float alpha, hipStream_t s);
+
+// Leading dimension of the internal ping-pong buffers.  A random row gather costs 128-B line
+// requests, not bytes, so rows are padded to start on a line
+// (next power of two up to one line, then whole lines) -- but only when that lowers the
+// average number of lines a row spans; otherwise (e.g. 400-B fp32 rows: 4 lines either way)
+// packed rows avoid a partially written line per row.
+inline double avg_lines(int64_t row_bytes, int64_t stride) {
+  // rows start at offsets (i * stride) mod 128, periodic
+  int64_t g = stride % 128 == 0 ? 128 : stride;
+  int64_t a = 128, b = g;
+  while (b) { const int64_t t = a % b; a = b; b = t; }
+  const int64_t period = 128 / a;
+  double sum = 0.0;
+  for (int64_t i = 0; i < period; ++i) {
+    const int64_t o = (i * stride) % 128;
+    sum += (double)((o + row_bytes - 1) / 128 + 1);
+  }
+  return sum / (double)period;
+}
+
+inline int64_t line_ld(int64_t f, int dtype) {
+  const int64_t es = dtype == APPNP_F32 ? 4 : 2;
+  const int64_t line = 128 / es;
+  if (f <= 0) return 1;
+  int64_t padded;
+  if (f <= line) {
+    padded = 1;
+    while (padded < f) padded <<= 1;
+  } else {
+    padded = (f + line - 1) / line * line;
+  }
+  const int64_t v = es == 4 ? 4 : 8;  // keep 16-B vectors possible for the packed layout
+  const int64_t packed = (f + v - 1) / v * v;
+  return avg_lines(f * es, padded * es) < avg_lines(f * es, packed * es) ? padded : packed;
+}
 
 }  // namespace appnp

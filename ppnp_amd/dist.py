@@ -477,6 +477,106 @@ def _hip_step(runner: PartitionedAPPNP, src, out_rows, k, part):
              seed=runner.seed)
 
 
+class NativeRowAPPNP:
+    """The north_star's row partition run by the library's own loop (appnp_dist_*,
+    include/ppnp_amd.h): the engine a C/C++ caller gets from the ABI.  This class only drives it
+    from Python.  It makes the same launches as ``PartitionedAPPNP`` on a ``Layout(P, 1)``, but
+    the K loop, the overlap schedule and the exchange stream live in C++.
+
+    exchange: 'rccl' -- appnp_allgather_rccl on torch's own communicator (the process group's
+    ncclComm_t, so RCCL is called from C with no Python per iteration); 'gloo' -- a Python
+    callback that stages the shards through host memory (tests: ranks sharing one GPU).
+    Default: 'rccl' on an 'nccl' process group, else 'gloo'.  Collective: every rank builds
+    and runs it with the same arguments."""
+
+    def __init__(self, indptr, indices, n, device, overlap=True, mode="sym", data=None,
+                 exchange=None, rank=None, world=None):
+        import ctypes as C
+
+        lib = _lib.load()
+        self.device = torch.device(device)
+        self.rank = dist.get_rank() if rank is None else rank
+        self.world = dist.get_world_size() if world is None else world
+        backend = dist.get_backend() if dist.is_initialized() else None
+        self.exchange = exchange or ("rccl" if backend == "nccl" else "gloo")
+        self._ws = None
+        ctx = None
+        if self.world == 1:
+            fn = None
+        elif self.exchange == "rccl":
+            pg = dist.distributed_c10d._get_default_group()
+            ctx = C.c_void_p(pg._get_backend(self.device)._comm_ptr())
+            fn = _lib.ALLGATHER_FN(C.cast(lib.appnp_allgather_rccl, C.c_void_p).value)
+        elif self.exchange == "gloo":
+            fn = _lib.ALLGATHER_FN(self._gloo_allgather)
+        else:
+            raise ValueError(f"unknown exchange {exchange!r}")
+        self._fn = fn  # the ctypes callback must outlive the handle
+        self._ctx = ctx
+        ip = indptr.to(self.device, torch.int32).contiguous()
+        ix = indices.to(self.device, torch.int32).contiguous()
+        val = None if data is None else data.to(self.device, torch.float32).contiguous()
+        h = C.c_void_p()
+        stream = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        _lib.check("appnp_dist_create", lib.appnp_dist_create(
+            C.c_void_p(ip.data_ptr()), C.c_void_p(ix.data_ptr()) if ix.numel() else None,
+            C.c_void_p(val.data_ptr()) if val is not None and val.numel() else None, n,
+            ix.numel(), _lib.NORM[mode], self.rank, self.world, int(bool(overlap)), fn, ctx,
+            stream, C.byref(h)))
+        self._h = h
+        lo, hi, shard = C.c_int64(), C.c_int64(), C.c_int64()
+        _lib.check("appnp_dist_rows", lib.appnp_dist_rows(h, C.byref(lo), C.byref(hi),
+                                                          C.byref(shard)))
+        self.n, self.lo, self.hi, self.shard = n, lo.value, hi.value, shard.value
+
+    def _gloo_allgather(self, buf, shard_bytes, rank, nranks, stream, ctx):
+        try:
+            torch.cuda.synchronize(self.device)
+            off = buf - self._ws.data_ptr()
+            view = self._ws[off:off + nranks * shard_bytes]
+            host = view.cpu()
+            parts = list(host.split(shard_bytes))
+            dist.all_gather(parts, parts[rank].clone())
+            view.copy_(host)
+            torch.cuda.synchronize(self.device)
+            return 0
+        except Exception:  # noqa: BLE001 -- no Python exception may cross the C frame
+            return _lib.APPNP_EDEVICE
+
+    def run(self, H_rows, K, alpha, p_drop=0.0, seed=0, out=None):
+        """This rank's rows of APPNP_K(H) from this rank's rows ``H_rows`` [hi - lo, F]."""
+        import ctypes as C
+
+        lib = _lib.load()
+        dtype = {torch.float32: _lib.F32, torch.bfloat16: _lib.BF16}[H_rows.dtype]
+        f = int(H_rows.shape[1])
+        if H_rows.stride(1) != 1:
+            H_rows = H_rows.contiguous()
+        Z = out if out is not None else torch.empty_like(H_rows)
+        need = lib.appnp_dist_workspace_bytes(self._h, f, dtype)
+        if self._ws is None or self._ws.numel() < need:
+            self._ws = torch.empty(max(need, 1), dtype=torch.uint8, device=self.device)
+        rows = self.hi - self.lo
+        ptr = (lambda t: C.c_void_p(t.data_ptr()) if rows > 0 else None)
+        _lib.check("appnp_dist_propagate", lib.appnp_dist_propagate(
+            self._h, ptr(H_rows), max(H_rows.stride(0), f), ptr(Z), max(Z.stride(0), f), f,
+            dtype, int(K), float(alpha), float(p_drop), int(seed) & (2**64 - 1),
+            C.c_void_p(self._ws.data_ptr()), self._ws.numel(),
+            C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)))
+        return Z
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.load().appnp_dist_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+
 INT32_MAX = 2**31 - 1
 
 

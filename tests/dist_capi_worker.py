@@ -1,0 +1,92 @@
+#!/usr/bin/env python
+"""End-to-end check of the library's own row-partitioned loop (appnp_dist_*, the C engine
+behind ppnp_amd.dist.NativeRowAPPNP) on real HIP kernels.
+
+    torchrun --nproc-per-node P --master-addr 127.0.0.1 tests/dist_capi_worker.py
+        [--workload pubmed-synth] [--overlap] [--p-drop 0.3] [--dtype f32|bf16]
+
+Every rank propagates its rows through appnp_dist_propagate and compares them with the
+single-GPU appnp_propagate of the whole graph on its own device.  Backend gloo (the ranks may
+share one GPU; the exchange callback stages the shards through host memory), or nccl with
+PPNP_DIST_BACKEND=nccl: then the exchange is appnp_allgather_rccl on torch's own
+communicator, and at world size 1 the worker also calls appnp_allgather_rccl directly once,
+which checks that the library resolves the process's RCCL.  Exit status 1 on mismatch.
+"""
+
+import argparse
+import ctypes as C
+import os
+import sys
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--workload", default="pubmed-synth")
+    p.add_argument("--features", type=int, default=None)
+    p.add_argument("--overlap", action="store_true")
+    p.add_argument("--p-drop", type=float, default=0.0)
+    p.add_argument("--dtype", default="f32", choices=["f32", "bf16"])
+    a = p.parse_args()
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
+    torch.cuda.set_device(dev)
+
+    import ppnp_amd
+    from ppnp_amd import _lib, synth
+    from ppnp_amd import dist as pdist
+
+    backend = os.environ.get("PPNP_DIST_BACKEND", "gloo")
+    if backend == "nccl":
+        dist.init_process_group("nccl", device_id=dev)
+    else:
+        dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    n, m, F, K, alpha, _ = synth.CONFIGS[a.workload]
+    F = a.features or F
+    dtype = torch.bfloat16 if a.dtype == "bf16" else torch.float32
+    indptr, indices = synth.graph_for(a.workload, device=dev)
+    H = synth.features(n, F, dtype=dtype, device=dev, seed=1)
+
+    runner = pdist.NativeRowAPPNP(indptr, indices, n, dev, overlap=a.overlap)
+    Z = runner.run(H[runner.lo:runner.hi], K, alpha, p_drop=a.p_drop, seed=5)
+    torch.cuda.synchronize()
+    G = ppnp_amd.Graph.from_csr(indptr, indices, None, n, device=dev)
+    ref = ppnp_amd.propagate_forward(G, H, K, alpha, p_drop=a.p_drop, seed=5)
+    block = ref[runner.lo:runner.hi]
+    err = (Z.double() - block.double()).abs().max().item() if block.numel() else 0.0
+    scale = ref.abs().max().item()
+    tol = (1e-5 if dtype == torch.float32 else 1e-2) * scale + 1e-6
+    ok = err <= tol
+    extra = ""
+    if backend == "nccl" and world == 1:
+        # the library's RCCL callback on torch's communicator: a one-rank in-place all-gather
+        lib = _lib.load()
+        pg = dist.distributed_c10d._get_default_group()
+        comm = pg._get_backend(dev)._comm_ptr()
+        buf = torch.arange(1024, dtype=torch.float32, device=dev)
+        before = buf.clone()
+        rc = lib.appnp_allgather_rccl(C.c_void_p(buf.data_ptr()), buf.numel() * 4, 0, 1,
+                                      C.c_void_p(torch.cuda.current_stream(dev).cuda_stream),
+                                      C.c_void_p(comm))
+        torch.cuda.synchronize()
+        ok = ok and rc == 0 and torch.equal(buf, before)
+        extra = f" rccl_callback rc={rc}"
+    runner.close()
+    print(f"[dist_capi] rank {rank}/{world} backend={dist.get_backend()} "
+          f"exchange={runner.exchange} overlap={a.overlap} dtype={a.dtype} p_drop={a.p_drop} "
+          f"rows [{runner.lo},{runner.hi}) max err {err:.3e} tol {tol:.3e}{extra} -> "
+          f"{'OK' if ok else 'FAIL'}", flush=True)
+    flag = torch.tensor([0 if ok else 1], dtype=torch.int64,
+                        device=dev if dist.get_backend() == "nccl" else "cpu")
+    dist.all_reduce(flag)
+    dist.destroy_process_group()
+    sys.exit(1 if flag.item() else 0)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,192 @@
+/*
+ * dist_smoke.c -- the row-partitioned engine (appnp_dist_*) from plain C, no Python, no torch.
+ *
+ * Two ranks are two threads sharing the one GPU.  Each thread has its own stream and
+ * appnp_dist handle, and the exchange callback is an in-process all-gather: drain the stream,
+ * barrier, copy every peer's shard out of the peer's buffer, drain, barrier.  Each rank's rows
+ * of Z_K are compared with appnp_propagate of the whole graph.  Cases: overlap (local columns
+ * while the exchange runs) and plain, with and without edge dropout.  Built by
+ * tests/test_native.py with gcc; run on the GPU box.  Exit status 0 on success.
+ */
+#define _POSIX_C_SOURCE 200809L
+#include <hip/hip_runtime_api.h>
+#include <math.h>
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "ppnp_amd.h"
+
+enum { P = 2, N = 3001, F = 12, K = 10, DEG = 4 };
+
+struct world {
+  pthread_barrier_t bar;
+  void* bufs[P];  /* each rank's current exchange buffer */
+};
+
+struct rank_ctx {
+  struct world* w;
+  int rank, overlap;
+  float p_drop;
+  const int32_t *d_ip, *d_ix;
+  int64_t nnz;
+  const float* d_H; /* all rows of H (the rank passes its own rows) */
+  float* d_Zref;    /* single-GPU result */
+  int rc;
+  double err;
+};
+
+static int exchange(void* buf, size_t shard_bytes, int rank, int nranks, void* stream,
+                    void* ctx) {
+  struct world* w = (struct world*)ctx;
+  hipStream_t s = (hipStream_t)stream;
+  if (hipStreamSynchronize(s) != hipSuccess) return APPNP_EDEVICE;  /* own shard complete */
+  w->bufs[rank] = buf;
+  pthread_barrier_wait(&w->bar);
+  for (int p = 0; p < nranks; ++p) {
+    if (p == rank) continue;
+    const size_t off = (size_t)p * shard_bytes;
+    if (hipMemcpyAsync((char*)buf + off, (char*)w->bufs[p] + off, shard_bytes,
+                       hipMemcpyDeviceToDevice, s) != hipSuccess)
+      return APPNP_EDEVICE;
+  }
+  if (hipStreamSynchronize(s) != hipSuccess) return APPNP_EDEVICE;
+  pthread_barrier_wait(&w->bar);  /* no rank writes its buffer again before every copy ends */
+  return APPNP_OK;
+}
+
+static void* run_rank(void* arg) {
+  struct rank_ctx* c = (struct rank_ctx*)arg;
+  hipStream_t s;
+  appnp_dist* d = NULL;
+  c->rc = -1;
+  if (hipStreamCreate(&s) != hipSuccess) return NULL;
+  int rc = appnp_dist_create(c->d_ip, c->d_ix, NULL, N, c->nnz, APPNP_NORM_SYM, c->rank, P,
+                             c->overlap, exchange, c->w, s, &d);
+  if (rc != APPNP_OK) { c->rc = rc; return NULL; }
+  int64_t lo, hi, shard;
+  appnp_dist_rows(d, &lo, &hi, &shard);
+  const size_t ws_bytes = appnp_dist_workspace_bytes(d, F, APPNP_F32);
+  void* ws = NULL;
+  float* d_Z = NULL;
+  if (hipMalloc(&ws, ws_bytes) != hipSuccess ||
+      hipMalloc((void**)&d_Z, (size_t)(hi - lo) * F * 4) != hipSuccess) {
+    c->rc = APPNP_ENOMEM;
+    return NULL;
+  }
+  rc = appnp_dist_propagate(d, c->d_H + lo * F, F, d_Z, F, F, APPNP_F32, K, 0.1f, c->p_drop, 77,
+                            ws, ws_bytes, s);
+  if (rc == APPNP_OK && hipStreamSynchronize(s) != hipSuccess) rc = APPNP_EDEVICE;
+  if (rc == APPNP_OK) {
+    const size_t cnt = (size_t)(hi - lo) * F;
+    float* z = (float*)malloc(cnt * 4);
+    float* r = (float*)malloc(cnt * 4);
+    hipMemcpy(z, d_Z, cnt * 4, hipMemcpyDeviceToHost);
+    hipMemcpy(r, c->d_Zref + lo * F, cnt * 4, hipMemcpyDeviceToHost);
+    double e = 0.0;
+    for (size_t i = 0; i < cnt; ++i) e = fmax(e, fabs((double)z[i] - (double)r[i]));
+    c->err = e;
+    free(z);
+    free(r);
+  }
+  c->rc = rc;
+  hipFree(ws);
+  hipFree(d_Z);
+  appnp_dist_destroy(d);
+  hipStreamDestroy(s);
+  return NULL;
+}
+
+int main(void) {
+  /* a ring plus DEG-2 pseudo-random chords per node, symmetrised, sorted */
+  static int32_t adj[N][2 * DEG];
+  static int cnt[N];
+  unsigned long long st = 12345;
+  for (int i = 0; i < N; ++i) {
+    int js[DEG];
+    js[0] = (i + 1) % N;
+    for (int t = 1; t < DEG - 1; ++t) {
+      st = st * 6364136223846793005ull + 1442695040888963407ull;
+      js[t] = (int)((st >> 33) % N);
+    }
+    for (int t = 0; t < DEG - 1; ++t) {
+      const int j = js[t];
+      if (j == i) continue;
+      int dup = 0;
+      for (int q = 0; q < cnt[i]; ++q) dup |= adj[i][q] == j;
+      if (dup || cnt[i] >= 2 * DEG || cnt[j] >= 2 * DEG) continue;
+      adj[i][cnt[i]++] = j;
+      adj[j][cnt[j]++] = i;
+    }
+  }
+  int32_t* indptr = (int32_t*)malloc((N + 1) * 4);
+  int32_t* indices = (int32_t*)malloc((size_t)N * 2 * DEG * 4);
+  int64_t nnz = 0;
+  for (int i = 0; i < N; ++i) {
+    indptr[i] = (int32_t)nnz;
+    for (int a = 1; a < cnt[i]; ++a)  /* insertion sort of the row */
+      for (int b = a; b > 0 && adj[i][b - 1] > adj[i][b]; --b) {
+        const int32_t t = adj[i][b];
+        adj[i][b] = adj[i][b - 1];
+        adj[i][b - 1] = t;
+      }
+    for (int a = 0; a < cnt[i]; ++a) indices[nnz++] = adj[i][a];
+  }
+  indptr[N] = (int32_t)nnz;
+  float* H = (float*)malloc((size_t)N * F * 4);
+  for (int i = 0; i < N * F; ++i) H[i] = (float)((i * 7919) % 2001 - 1000) / 1000.0f;
+
+  int32_t *d_ip, *d_ix;
+  float *d_H, *d_Zref;
+  void* d_ws;
+  if (hipMalloc((void**)&d_ip, (N + 1) * 4) || hipMalloc((void**)&d_ix, nnz * 4) ||
+      hipMalloc((void**)&d_H, (size_t)N * F * 4) || hipMalloc((void**)&d_Zref, (size_t)N * F * 4))
+    return 2;
+  hipMemcpy(d_ip, indptr, (N + 1) * 4, hipMemcpyHostToDevice);
+  hipMemcpy(d_ix, indices, nnz * 4, hipMemcpyHostToDevice);
+  hipMemcpy(d_H, H, (size_t)N * F * 4, hipMemcpyHostToDevice);
+  appnp_graph* g = NULL;
+  if (appnp_graph_create(d_ip, d_ix, NULL, N, nnz, APPNP_NORM_SYM, NULL, &g) != APPNP_OK) return 3;
+  const size_t ws_bytes = appnp_workspace_bytes(g, F, F, APPNP_F32);
+  if (hipMalloc(&d_ws, ws_bytes ? ws_bytes : 1)) return 2;
+
+  int failures = 0;
+  const float drops[2] = {0.0f, 0.25f};
+  for (int overlap = 0; overlap <= 1; ++overlap)
+    for (int di = 0; di < 2; ++di) {
+      if (appnp_propagate(g, d_H, F, d_Zref, F, F, APPNP_F32, K, 0.1f, drops[di], 77, d_ws,
+                          ws_bytes, NULL) != APPNP_OK ||
+          hipDeviceSynchronize() != hipSuccess)
+        return 4;
+      struct world w;
+      memset(&w, 0, sizeof(w));
+      pthread_barrier_init(&w.bar, NULL, P);
+      pthread_t th[P];
+      struct rank_ctx c[P];
+      for (int r = 0; r < P; ++r) {
+        c[r] = (struct rank_ctx){&w, r, overlap, drops[di], d_ip, d_ix, nnz, d_H, d_Zref, -1, 0.0};
+        pthread_create(&th[r], NULL, run_rank, &c[r]);
+      }
+      for (int r = 0; r < P; ++r) pthread_join(th[r], NULL);
+      pthread_barrier_destroy(&w.bar);
+      for (int r = 0; r < P; ++r) {
+        const int ok = c[r].rc == APPNP_OK && c[r].err <= 1e-5;
+        printf("rank %d overlap %d p_drop %.2f: rc %d max err %.3e %s\n", r, overlap, drops[di],
+               c[r].rc, c[r].err, ok ? "ok" : "FAIL");
+        failures += !ok;
+      }
+    }
+  appnp_graph_destroy(g);
+  hipFree(d_ip);
+  hipFree(d_ix);
+  hipFree(d_H);
+  hipFree(d_Zref);
+  hipFree(d_ws);
+  free(indptr);
+  free(indices);
+  free(H);
+  if (failures) return 5;
+  printf("dist_smoke ok\n");
+  return 0;
+}

@@ -65,6 +65,21 @@ def test_argument_validation_without_device():
     assert lib.appnp_step(None, 0, None, 0, None, 0, None, 0, None, 0, 1, 0, 0, 0.1, 0.0, 0, None) == _lib.APPNP_EINVAL
     assert lib.appnp_workspace_bytes(None, 10, 10, 0) == 0
     lib.appnp_graph_destroy(None)  # no-op
+    # the row-partitioned engine: validation before any device work
+    h = C.c_void_p()
+    assert lib.appnp_dist_create(None, None, None, 10, 0, 0, 0, 2, 1, None, None, None,
+                                 C.byref(h)) == _lib.APPNP_EINVAL  # 2 ranks, no exchange
+    assert lib.appnp_dist_create(None, None, None, 10, 0, 0, 2, 2, 0, None, None, None,
+                                 C.byref(h)) == _lib.APPNP_EINVAL  # rank out of range
+    assert lib.appnp_dist_create(None, None, None, 10, 0, 0, 0, 1, 0, None, None, None,
+                                 None) == _lib.APPNP_EINVAL
+    assert lib.appnp_dist_propagate(None, None, 0, None, 0, 1, 0, 1, 0.1, 0.0, 0, None, 0,
+                                    None) == _lib.APPNP_EINVAL
+    assert lib.appnp_dist_rows(None, None, None, None) == _lib.APPNP_EINVAL
+    assert lib.appnp_dist_graph(None) is None
+    assert lib.appnp_dist_workspace_bytes(None, 10, 0) == 0
+    assert lib.appnp_allgather_rccl(None, 16, 0, 1, None, None) == _lib.APPNP_EINVAL
+    lib.appnp_dist_destroy(None)  # no-op
 
 
 def test_no_cpu_fallback_when_library_missing(tmp_path, monkeypatch):

@@ -170,3 +170,35 @@ def test_bench_two_ranks_autotune_and_parity():
     assert res["parity"]["ok"], res["parity"]
     tried = res["config"]["autotune_ms_per_step"]
     assert len(tried) >= 2 and all(v is not None for v in tried.values()), tried
+
+
+@pytest.mark.parametrize("ranks,extra", [
+    (2, ["--overlap"]), (2, []), (3, ["--overlap", "--p-drop", "0.3"]),
+    (2, ["--dtype", "bf16"]), (4, ["--workload", "arxiv-synth", "--overlap"])])
+def test_native_row_engine_matches_single_gpu(ranks, extra):
+    """The library's own row-partitioned loop (appnp_dist_create / appnp_dist_propagate: the
+    C engine of SURVEY.md 8(b)) over 2-4 ranks sharing the GPU, with the exchange supplied
+    as a host-staged gloo callback, against the single-GPU appnp_propagate."""
+    env = dict(os.environ, PPNP_DIST_BACKEND="gloo", PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={ranks}", "--master-addr=127.0.0.1",
+           f"--master-port={_free_port()}", os.path.join(ROOT, "tests", "dist_capi_worker.py"),
+           *extra]
+    proc = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=110)
+    lines = [l for l in proc.stdout.splitlines() if l.startswith("[dist_capi]")]
+    assert proc.returncode == 0, proc.stdout[-3000:] + proc.stderr[-3000:]
+    assert len(lines) == ranks and all(l.endswith("OK") for l in lines), lines
+
+
+def test_native_row_engine_rccl_callback_one_rank():
+    """appnp_allgather_rccl resolves the RCCL PyTorch loaded and runs on its communicator
+    (one rank: RCCL refuses two ranks on one device), and the engine's one-rank run agrees
+    with appnp_propagate."""
+    env = dict(os.environ, PPNP_DIST_BACKEND="nccl", PYTHONPATH=ROOT)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.join(ROOT, "tests", "dist_capi_worker.py")]
+    proc = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=110)
+    lines = [l for l in proc.stdout.splitlines() if l.startswith("[dist_capi]")]
+    assert proc.returncode == 0, proc.stdout[-3000:] + proc.stderr[-3000:]
+    assert len(lines) == 1 and "rccl_callback rc=0" in lines[0] and lines[0].endswith("OK"), lines
