@@ -165,7 +165,8 @@ def tune_layouts(cands, indptr, indices, n, H, K, alpha, dev, ctl, reps=2):
     best, best_ms, times = None, None, {}
     for layout, overlap, exchange in cands:
         name = (f"rows{layout.rows}xcols{layout.cols}" + ("-overlap" if overlap else "")
-                + (f"-{exchange}" if layout.rows > 1 and layout.cols > 1 else ""))
+                + (f"-{exchange}" if (layout.rows > 1 and layout.cols > 1)
+                   or exchange == "native" else ""))
         if torch.distributed.get_rank() == 0:
             log(f"[bench] autotune: building {layout} overlap={overlap} exchange={exchange}")
         r, err, dt = None, "", 0.0
@@ -414,8 +415,8 @@ def main():
     rows_per_s = n * K * args.steps / wall  # also N*K/t
     parallelism = ((f"rows{runner.layout.rows}xcols{runner.layout.cols}"
                     + ("-overlap" if runner.overlap else "")
-                    + (f"-{runner.exchange}" if runner.layout.rows > 1 and runner.layout.cols > 1
-                       and runner.exchange != "none" else "")
+                    + (f"-{runner.exchange}" if (runner.layout.rows > 1 and runner.layout.cols > 1
+                       and runner.exchange != "none") or runner.exchange == "native" else "")
                     + (f"-EMULATED-rank{args.emulate}" if args.emulate else ""))
                    if distributed else "single")
     traffic = committed_traffic(args.workload, dtype, parallelism)

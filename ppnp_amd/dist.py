@@ -350,7 +350,8 @@ class PartitionedAPPNP:
         """rank / world override the process group's (single-GPU emulation of one rank of a
         larger layout, with a ``NullComm``: measures that rank's kernel time only).
         exchange: 'multipath' (MultipathComm, R x C layouts with C > 1) or 'group' (one RCCL
-        all-gather per column group); a pure row layout always uses the all-gather."""
+        all-gather per column group); a pure row layout always uses the all-gather, or, with
+        'native', the library's own loop (NativeRowRunner over appnp_dist_*)."""
         if rank is None:
             rank = dist.get_rank() if dist.is_initialized() else 0
         if world is None:
@@ -358,6 +359,11 @@ class PartitionedAPPNP:
         layout = layout or Layout(1, world)
         if layout.size != world:
             raise ValueError("layout does not match the world size")
+        if exchange == "native":  # the library's own row loop (appnp_dist_*)
+            if layout.cols != 1 or comm is not None or step_fn is not None or graph_fn is not None:
+                raise ValueError("exchange='native' runs a pure row layout on the HIP path")
+            return NativeRowRunner(indptr, indices, n, H, K, alpha, device, overlap=overlap,
+                                   mode=mode, data=data, p_drop=p_drop, seed=seed)
         ri, ci = layout.coords(rank)
         f = int(H.shape[1])
         lo, hi, shard = row_range(n, layout.rows, ri)
@@ -577,6 +583,53 @@ class NativeRowAPPNP:
             pass
 
 
+class _DistGraphInfo:
+    """The held rows' sizes of an appnp_dist graph (what bench.py reads from runner.graph)."""
+
+    def __init__(self, handle):
+        import ctypes as C
+
+        n, lo, hi, nnz = C.c_int64(), C.c_int64(), C.c_int64(), C.c_int64()
+        mode, sym = C.c_int(), C.c_int()
+        _lib.check("appnp_graph_info", _lib.load().appnp_graph_info(
+            handle, C.byref(n), C.byref(lo), C.byref(hi), C.byref(nnz), C.byref(mode),
+            C.byref(sym)))
+        self.n, self.row_lo, self.row_hi = n.value, lo.value, hi.value
+        self.rows = hi.value - lo.value
+        self.nnz_hat = nnz.value
+
+
+class NativeRowRunner:
+    """``PartitionedAPPNP``'s runner surface (run(), out, lo/hi, layout, graph) over
+    ``NativeRowAPPNP``: how bench.py times the library's own row loop as a layout candidate
+    (exchange 'native')."""
+
+    exchange = "native"
+
+    def __init__(self, indptr, indices, n, H, K, alpha, device, overlap=True, mode="sym",
+                 data=None, p_drop=0.0, seed=0):
+        self.engine = NativeRowAPPNP(indptr, indices, n, device, overlap=overlap, mode=mode,
+                                     data=data)
+        self.layout = Layout(self.engine.world, 1)
+        self.rank = self.engine.rank
+        self.overlap = bool(overlap and self.engine.world > 1)
+        self.lo, self.hi = self.engine.lo, self.engine.hi
+        self.f_lo, self.f_hi = 0, int(H.shape[1])
+        self.H = H[self.lo:self.hi].to(device).contiguous()
+        self.K, self.alpha, self.p_drop, self.seed = K, alpha, p_drop, seed
+        self.out = torch.empty_like(self.H)
+        import ctypes as C
+
+        self.graph = _DistGraphInfo(C.c_void_p(_lib.load().appnp_dist_graph(self.engine._h)))
+
+    @property
+    def width(self) -> int:
+        return self.f_hi - self.f_lo
+
+    def run(self):
+        return self.engine.run(self.H, self.K, self.alpha, self.p_drop, self.seed, out=self.out)
+
+
 INT32_MAX = 2**31 - 1
 
 
@@ -627,7 +680,7 @@ def candidate_layouts(world: int, f: int, n: int = 0, nnz_hat: int = 0, elem_byt
     row = Layout(world, 1)
     # the north_star's design -- a pure row partition, all-gather overlapped with the local
     # product -- is always timed when it fits, so the scaling run measures it next to the rest
-    row_cand = ([(row, True, "group")]
+    row_cand = ([(row, True, "group"), (row, True, "native")]
                 if world >= 2 and fits(row, n, f, nnz_hat, elem_bytes, True, mem_bytes) else [])
     if first.rows > 1:  # row groups forced by size: overlap the exchange, try both routes
         cands = ([(first, True, "multipath"), (first, True, "group")] if first.cols > 1 else

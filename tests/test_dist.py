@@ -124,12 +124,14 @@ def test_layout_helpers():
     assert choose_layout(8, 2_449_029, 100, 126_000_000) == Layout(1, 8)
     from ppnp_amd.dist import candidate_layouts
 
-    # the north_star's pure row partition (overlapped all-gather) is timed at every N >= 2
+    # the north_star's pure row partition (overlapped all-gather) is timed at every N >= 2,
+    # driven from Python and by the library's own loop (appnp_dist_*)
     assert candidate_layouts(2, 100) == [(Layout(1, 2), False, "group"),
-                                         (Layout(2, 1), True, "group")]
+                                         (Layout(2, 1), True, "group"),
+                                         (Layout(2, 1), True, "native")]
     c8 = candidate_layouts(8, 100)
     assert c8[0] == (Layout(1, 8), False, "group") and (Layout(2, 4), True, "multipath") in c8
-    assert (Layout(8, 1), True, "group") in c8
+    assert (Layout(8, 1), True, "group") in c8 and (Layout(8, 1), True, "native") in c8
 
 
 def test_layout_memory_and_index_limits():
@@ -148,7 +150,7 @@ def test_layout_memory_and_index_limits():
     assert choose_layout(8, n2, 128, nnz2, 4, 288 * gb) == Layout(2, 4)
     assert candidate_layouts(8, 128, n2, nnz2, 4, 288 * gb) == [
         (Layout(2, 4), True, "multipath"), (Layout(2, 4), True, "group"),
-        (Layout(8, 1), True, "group")]
+        (Layout(8, 1), True, "group"), (Layout(8, 1), True, "native")]
     # row groups split the CSR, column groups split Z: 2x4 holds the smallest share here
     shares = {lay: rank_bytes(lay, n, 100, nnz) for lay in
               (Layout(1, 8), Layout(2, 4), Layout(4, 2), Layout(8, 1))}
