@@ -75,7 +75,8 @@ struct RemLayout {
 // it comes from a lane of the same row index (segment); rows are sorted, so equality of the
 // two end points means every lane between belongs to the segment too.
 constexpr int kDppRowShr1 = 0x111, kDppRowShr2 = 0x112, kDppRowShr4 = 0x114,
-              kDppRowShr8 = 0x118, kDppRowBcast15 = 0x142, kDppRowBcast31 = 0x143;
+              kDppRowShr8 = 0x118, kDppRowBcast15 = 0x142, kDppRowBcast31 = 0x143,
+              kDppWaveShr1 = 0x138;  // whole-wave shift by one lane (GFX9 family)
 
 template <int CTRL, int ROW_MASK>
 __device__ __forceinline__ void seg_step(int row, f32x4& v) {
@@ -96,13 +97,31 @@ __device__ __forceinline__ void seg_step(int row, f32x4& v) {
   }
 }
 
-__device__ __forceinline__ void seg_scan(int row, f32x4& v) {
-  seg_step<kDppRowShr1, 0xf>(row, v);
-  seg_step<kDppRowShr2, 0xf>(row, v);
-  seg_step<kDppRowShr4, 0xf>(row, v);
-  seg_step<kDppRowShr8, 0xf>(row, v);
-  seg_step<kDppRowBcast15, 0xa>(row, v);  // rows 1, 3 <- lanes 15, 47
-  seg_step<kDppRowBcast31, 0xc>(row, v);  // rows 2, 3 <- lane 31
+// Segmented inclusive scan of v over runs of equal `row` (Hillis-Steele over DPP: row_shr 1,
+// 2, 4, 8 within each 16-lane row, then row_bcast15 / row_bcast31 across rows), running only
+// the steps some run needs.  `heads` (wave-uniform) marks the first lane of every run.  An
+// in-row step of shift d is a no-op unless some lane sits >= d places after its run's head
+// within its 16-lane row, and a broadcast is a no-op unless lane 16 / 48 (bcast15) or lane 32
+// (bcast31) continues a run.  So the result is the full six-step scan's, bit for bit.  Runs in
+// a chunk are short (a group's row has ~0.7 entries per source block), so most chunks need
+// two or three steps.
+__device__ __forceinline__ void seg_scan(int row, f32x4& v, unsigned long long heads) {
+  unsigned long long m = ~(heads | 0x0001000100010001ull);  // lanes >= 1 after their head
+  if (m) {
+    seg_step<kDppRowShr1, 0xf>(row, v);
+    m &= m << 1;  // >= 2 after
+    if (m) {
+      seg_step<kDppRowShr2, 0xf>(row, v);
+      m &= m << 2;  // >= 4 after
+      if (m) {
+        seg_step<kDppRowShr4, 0xf>(row, v);
+        if (m & (m << 4)) seg_step<kDppRowShr8, 0xf>(row, v);
+      }
+    }
+  }
+  if (~heads & ((1ull << 16) | (1ull << 48)))
+    seg_step<kDppRowBcast15, 0xa>(row, v);  // rows 1, 3 <- lanes 15, 47
+  if (~heads & (1ull << 32)) seg_step<kDppRowBcast31, 0xc>(row, v);  // rows 2, 3 <- lane 31
 }
 
 // Epilogue of one row of the iteration: FWD out[i, :nv] = (1-alpha) R[i] + alpha H_rem[i]
@@ -200,9 +219,10 @@ __global__ __launch_bounds__(kRemThreads) void k_rem_persist(StepArgs a, RemLayo
         const float w =
             act ? edge_weight(wt[u], r0 + row, (int32_t)(cbase[u] + (en[u] & cmask)), a) : 0.0f;
         f32x4 v = f32x4{w * zv[u].x, w * zv[u].y, w * zv[u].z, w * zv[u].w};
-        seg_scan(row, v);
-        const int prev = __shfl_up(row, 1);
-        const unsigned long long heads = __ballot(lane == 0 || prev != row);
+        // the previous lane's row (lane 0: none), by DPP rather than an LDS permute
+        const int prev = __builtin_amdgcn_update_dpp(-1, row, kDppWaveShr1, 0xf, 0xf, false);
+        const unsigned long long heads = __ballot(lane == 0 || prev != row || !act);
+        seg_scan(row, v, heads);
         const bool tail = lane == kWave - 1 || ((heads >> (lane + 1)) & 1ull);
         if (act && tail) {
           const f32x4 c = acc[row];
