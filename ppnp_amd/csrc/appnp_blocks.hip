@@ -40,6 +40,11 @@
 // packed as (row in group << 20 | column in block) with their fp32 value; padding entries are
 // all ones with value 0.  off holds passes x (CUs x 16) x blocks + 1 ints: linear in n
 // (one int per 640-row x 2^15-column tile of A_hat, ~1.2 MB on products-synth).
+//
+// A unit graph (unweighted A without self loops: every entry of A+I is 1, so A_hat_ij =
+// dl_i dr_j with sym: dl = dr = dinv, rw: dl = dinv, dr = 1) stores NO values: the remainder
+// buffers hold dr o Z_rem, the pass sums the gathered rows and the epilogue scales by dl_i.
+// The entry stream halves (4 B per entry): 0.91 -> 0.81 ms per products-synth launch.
 #include <algorithm>
 #include <cstdlib>
 
@@ -64,9 +69,13 @@ static_assert(kRemRowBits + kRemColBits == 32, "packed entry is 32 bits");
 struct RemLayout {
   const int32_t* off;   // segment starts, [(pass * slots + slot) * nb + block]
   const uint32_t* ent;  // packed (row in group, column in block); padding: kRemNone
-  const float* val;
+  const float* val;     // entry values; null for a unit graph (VF kernels)
   const int32_t* cblk;  // source block of each chunk of 64 entries
+  const float* dl;      // VF: row scale of A_hat (fp32 dinv)
+  const float* dr;      // VF: column scale (sym: fp32 dinv; rw: null).  Z_rem buffers hold
+                        // dr o Z_rem, so a gathered row needs no value
   int32_t nb, br_log2, slots, rg, passes;
+  int32_t scale_out;    // VF: the output is the next remainder buffer (store dr o y)
 };
 
 // ---- segmented inclusive scan over the 64 lanes (rows non-decreasing across lanes) --------
@@ -128,12 +137,19 @@ __device__ __forceinline__ void seg_scan(int row, f32x4& v, unsigned long long h
 // (a.h = H_rem, a.out / a.ld_out, a.f = nv valid columns: 4 into the next Z_rem, 1-4 into Z's
 // last columns); BWD G_k = (1-alpha) R into the next remainder buffer (none at k = 0) and
 // dH[:, fs:f] += alpha' G_k (a.rem_dh / a.ld_rem_dh).
-template <int EPI>
-__device__ __forceinline__ void rem_finish(const StepArgs& a, int64_t i, f32x4 acc) {
+template <int EPI, bool VF>
+__device__ __forceinline__ void rem_finish(const StepArgs& a, const RemLayout& L, int64_t i,
+                                           f32x4 acc) {
+  float so = 1.0f;  // VF: scale of a stored remainder row (dr_i), 1 for Z itself
+  if constexpr (VF) {
+    const float dl = L.dl[i];
+    acc = f32x4{dl * acc.x, dl * acc.y, dl * acc.z, dl * acc.w};
+    if (L.scale_out && L.dr) so = L.dr[i];
+  }
   if constexpr (EPI == EPI_BWD) {
     const float y[4] = {a.scale * acc.x, a.scale * acc.y, a.scale * acc.z, a.scale * acc.w};
     if (a.out)
-      static_cast<f32x4*>(a.out)[i] = f32x4{y[0], y[1], y[2], y[3]};
+      static_cast<f32x4*>(a.out)[i] = f32x4{so * y[0], so * y[1], so * y[2], so * y[3]};
     const int nv = a.f;
     float* d = a.rem_dh + i * a.ld_rem_dh;
     if (nv == 4) {
@@ -163,7 +179,7 @@ __device__ __forceinline__ void rem_finish(const StepArgs& a, int64_t i, f32x4 a
                         fmaf(a.alpha, nv > 3 ? h.w : 0.0f, a.scale * acc.w)};
     float* o = static_cast<float*>(a.out) + i * a.ld_out;
     if (nv == 4) {
-      *reinterpret_cast<f32x4*>(o) = f32x4{y[0], y[1], y[2], y[3]};
+      *reinterpret_cast<f32x4*>(o) = f32x4{so * y[0], so * y[1], so * y[2], so * y[3]};
     } else {
       for (int v = 0; v < nv; ++v) o[v] = y[v];
     }
@@ -171,8 +187,11 @@ __device__ __forceinline__ void rem_finish(const StepArgs& a, int64_t i, f32x4 a
 }
 
 // One iteration of the remainder columns over all source blocks (see the file comment).
-// a.zin = Z_rem (n x 4 fp32); U chunks of 64 entries in flight per wave.
-template <int EPI, int U>
+// a.zin = Z_rem (n x 4 fp32; VF: dr o Z_rem); U chunks of 64 entries in flight per wave.
+// VF (unit graph): entries carry no value -- the sum of the gathered dr_j Z_j is scaled by
+// dl_i in the epilogue, so the entry stream is 4 B per entry instead of 8 (0.91 -> 0.81 ms
+// per products-synth launch).
+template <int EPI, int U, bool VF>
 __global__ __launch_bounds__(kRemThreads) void k_rem_persist(StepArgs a, RemLayout L) {
   extern __shared__ f32x4 rem_acc[];
   const int lane = threadIdx.x & (kWave - 1);
@@ -191,34 +210,37 @@ __global__ __launch_bounds__(kRemThreads) void k_rem_persist(StepArgs a, RemLayo
     const int32_t c_end = L.off[(g + 1) * L.nb] / kRemChunk;
     for (int32_t c = L.off[g * L.nb] / kRemChunk; c < c_end; c += U) {
       const int nch = min(U, c_end - c);
-      int64_t cbase[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        cbase[u] = u < nch ? (int64_t)L.cblk[c + u] << L.br_log2 : 0;
+      int32_t cb[U];  // first source row of each chunk's block (wave-uniform: scalar loads)
       uint32_t en[U];
       float wt[U];
-      f32x4 zv[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
+        cb[u] = 0;
         en[u] = kRemNone;
-        wt[u] = 0.0f;
+        wt[u] = 1.0f;
         if (u < nch) {
           const int64_t e = (int64_t)(c + u) * kRemChunk + lane;
+          cb[u] = L.cblk[c + u] << L.br_log2;
           en[u] = ld_nt<uint32_t>(L.ent + e);
-          wt[u] = ld_nt<float>(L.val + e);
+          if constexpr (!VF) wt[u] = ld_nt<float>(L.val + e);
         }
       }
+      f32x4 zv[U];
 #pragma unroll
       for (int u = 0; u < U; ++u)
-        zv[u] = en[u] != kRemNone ? z[cbase[u] + (en[u] & cmask)] : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        zv[u] = en[u] != kRemNone ? z[cb[u] + (int32_t)(en[u] & cmask)]
+                                  : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if (u >= nch) break;  // wave-uniform
         const bool act = en[u] != kRemNone;
         const int row = (int)(en[u] >> kRemColBits);
-        const float w =
-            act ? edge_weight(wt[u], r0 + row, (int32_t)(cbase[u] + (en[u] & cmask)), a) : 0.0f;
-        f32x4 v = f32x4{w * zv[u].x, w * zv[u].y, w * zv[u].z, w * zv[u].w};
+        f32x4 v = zv[u];
+        if (!VF || a.drop_on) {
+          const float w =
+              act ? edge_weight(wt[u], r0 + row, cb[u] + (int32_t)(en[u] & cmask), a) : 0.0f;
+          v = f32x4{w * v.x, w * v.y, w * v.z, w * v.w};
+        }
         // the previous lane's row (lane 0: none), by DPP rather than an LDS permute
         const int prev = __builtin_amdgcn_update_dpp(-1, row, kDppWaveShr1, 0xf, 0xf, false);
         const unsigned long long heads = __ballot(lane == 0 || prev != row || !act);
@@ -230,7 +252,7 @@ __global__ __launch_bounds__(kRemThreads) void k_rem_persist(StepArgs a, RemLayo
         }
       }
     }
-    for (int r = lane; r < rows; r += kWave) rem_finish<EPI>(a, r0 + r, acc[r]);
+    for (int r = lane; r < rows; r += kWave) rem_finish<EPI, VF>(a, L, r0 + r, acc[r]);
   }
 }
 
@@ -278,7 +300,7 @@ __global__ __launch_bounds__(kBlock) void k_rb_walk(const int32_t* __restrict__ 
         if (act) {
           const int32_t pos = base + (lane - head);
           ent[pos] = ((uint32_t)(i - r0) << kRemColBits) | ((uint32_t)c & ((1u << br_log2) - 1u));
-          bval[pos] = val[e];
+          if (bval) bval[pos] = val[e];
         }
       } else {
         const int64_t d = (int64_t)c - i;
@@ -307,11 +329,12 @@ __global__ __launch_bounds__(kBlock) void k_rb_chunks(const int32_t* __restrict_
 }
 
 // H [n, ld_h] -> the split layout: main [n, fs] (whole lines per row) and rem [n, 4]
-// (columns fs..f-1, zero padded).  Thread per 16-B piece of a row (fs / 4 + 1 pieces).
+// (columns fs..f-1, zero padded; times rem_scale[row] when given).  Thread per 16-B piece of a row (fs / 4 + 1 pieces).
 __global__ __launch_bounds__(kBlock) void k_split_copy(const float* __restrict__ h, int64_t ld_h,
                                                        int64_t n, int f, int fs,
                                                        float* __restrict__ main,
-                                                       float* __restrict__ rem) {
+                                                       float* __restrict__ rem,
+                                                       const float* __restrict__ rem_scale) {
   const int pieces = fs / 4 + 1;
   const int64_t total = n * pieces;
   for (int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x; t < total;
@@ -336,20 +359,31 @@ __global__ __launch_bounds__(kBlock) void k_split_copy(const float* __restrict__
         if (nv > 1) v.y = p[1];
         if (nv > 2) v.z = p[2];
       }
+      if (rem_scale) {  // unit graph: the remainder buffers hold dr o Z_rem
+        const float d = rem_scale[row];
+        v = f32x4{d * v.x, d * v.y, d * v.z, d * v.w};
+      }
       *reinterpret_cast<f32x4*>(rem + row * 4) = v;
     }
   }
 }
 
-template <int EPI>
+template <int EPI, bool VF>
 hipError_t launch_rem(dim3 grid, dim3 block, size_t lds, hipStream_t s, const StepArgs& a,
                       const RemLayout& L) {
   static const hipError_t attr = hipFuncSetAttribute(  // > 64 KiB of dynamic LDS, once
-      reinterpret_cast<const void*>(k_rem_persist<EPI, kRemU>),
+      reinterpret_cast<const void*>(k_rem_persist<EPI, kRemU, VF>),
       hipFuncAttributeMaxDynamicSharedMemorySize, kRemLdsBytes);
   if (attr != hipSuccess) return attr;
-  hipLaunchKernelGGL((k_rem_persist<EPI, kRemU>), grid, block, lds, s, a, L);
+  hipLaunchKernelGGL((k_rem_persist<EPI, kRemU, VF>), grid, block, lds, s, a, L);
   return hipGetLastError();
+}
+
+// fp32 copy of dinv (the unit graph's row / column scales)
+__global__ __launch_bounds__(kBlock) void k_dinv_f32(const double* __restrict__ d, int64_t n,
+                                                     float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i < n) out[i] = (float)d[i];
 }
 
 int env_or(const char* name, int dflt) {
@@ -397,6 +431,9 @@ int graph_build_source_blocks(appnp_graph* g, hipStream_t s) {
                                                                        : APPNP_EDEVICE;
     return rc == APPNP_OK;
   };
+  // a unit graph (every entry of A+I is 1) stores no values: A_hat_ij = dl_i dr_j.
+  // APPNP_REM_VF=0 keeps the values (measurement)
+  const bool vf = g->unit && env_or("APPNP_REM_VF", 1) != 0;
   const int64_t n_groups = passes * slots;
   const unsigned grid = (unsigned)((n_groups + kWalkWaves - 1) / kWalkWaves);
   const size_t lds = (size_t)kWalkWaves * nb * sizeof(int32_t);
@@ -417,13 +454,21 @@ int graph_build_source_blocks(appnp_graph* g, hipStream_t s) {
     }
     const int64_t total = std::max<int64_t>(1, h_tot[0]);
     if (rc == APPNP_OK && ok(hipMalloc(&g->rb_ent, total * sizeof(uint32_t))) &&
-        ok(hipMalloc(&g->rb_val, total * sizeof(float))) &&
+        (vf || ok(hipMalloc(&g->rb_val, total * sizeof(float)))) &&
         ok(hipMemsetAsync(g->rb_ent, 0xff, total * sizeof(uint32_t), s)) &&  // kRemNone
-        ok(hipMemsetAsync(g->rb_val, 0, total * sizeof(float), s)) &&
+        (vf || ok(hipMemsetAsync(g->rb_val, 0, total * sizeof(float), s))) &&
+        (!vf || ok(hipMalloc(&g->rb_dl, rows * sizeof(float)))) &&
+        (!vf || g->mode != APPNP_NORM_SYM || ok(hipMalloc(&g->rb_dr, rows * sizeof(float)))) &&
         ok(hipMalloc(&g->rb_cblk, std::max<int64_t>(1, total / kRemChunk) * sizeof(int32_t)))) {
       hipLaunchKernelGGL(k_rb_walk<true>, dim3(grid), dim3(kBlock), lds, s, g->row_ptr, g->col,
                          g->val, rows, (int)rg, (int)nb, br_log2, n_groups, nullptr, g->rb_off,
                          g->rb_ent, g->rb_val, nullptr);
+      if (vf && ok(hipGetLastError())) {
+        const unsigned gb = (unsigned)((rows + kBlock - 1) / kBlock);
+        hipLaunchKernelGGL(k_dinv_f32, dim3(gb), dim3(kBlock), 0, s, g->dinv, rows, g->rb_dl);
+        if (g->rb_dr)
+          hipLaunchKernelGGL(k_dinv_f32, dim3(gb), dim3(kBlock), 0, s, g->dinv, rows, g->rb_dr);
+      }
       if (ok(hipGetLastError()))
         hipLaunchKernelGGL(k_rb_chunks, dim3((unsigned)((cells + kBlock - 1) / kBlock)),
                            dim3(kBlock), 0, s, g->rb_off, cells, (int)nb, g->rb_cblk);
@@ -439,6 +484,9 @@ int graph_build_source_blocks(appnp_graph* g, hipStream_t s) {
     if (g->rb_ent) (void)hipFree(g->rb_ent);
     if (g->rb_val) (void)hipFree(g->rb_val);
     if (g->rb_cblk) (void)hipFree(g->rb_cblk);
+    if (g->rb_dl) (void)hipFree(g->rb_dl);
+    if (g->rb_dr) (void)hipFree(g->rb_dr);
+    g->rb_dl = g->rb_dr = nullptr;
     g->rb_off = nullptr;
     g->rb_ent = nullptr;
     g->rb_val = nullptr;
@@ -462,7 +510,7 @@ int graph_build_source_blocks(appnp_graph* g, hipStream_t s) {
 // remainder columns, accumulated into; out (G_k's remainder) may be null.
 hipError_t launch_remainder(const appnp_graph* g, const StepArgs& a_in, int epi,
                             const float* z_rem, const float* h_rem, int64_t ld_h, float* out,
-                            int64_t ld_out, int nv, hipStream_t s) {
+                            int64_t ld_out, int nv, bool to_rem, hipStream_t s) {
   StepArgs a = a_in;
   a.zin = z_rem;
   a.aux = nullptr;
@@ -478,21 +526,25 @@ hipError_t launch_remainder(const appnp_graph* g, const StepArgs& a_in, int epi,
   a.ld_out = ld_out;
   a.f = nv;
   if (a.n_rows <= 0) return hipSuccess;
-  RemLayout L{g->rb_off, g->rb_ent, g->rb_val, g->rb_cblk, g->rb_nb, g->rb_br_log2, g->rb_slots, g->rb_rg,
-              g->rb_passes};
+  const bool vf = g->rb_val == nullptr;
+  RemLayout L{g->rb_off, g->rb_ent, g->rb_val, g->rb_cblk, g->rb_dl, g->rb_dr, g->rb_nb,
+              g->rb_br_log2, g->rb_slots, g->rb_rg, g->rb_passes, to_rem ? 1 : 0};
   const size_t lds = (size_t)kRemWaves * g->rb_rg * sizeof(f32x4);
   const dim3 grid((unsigned)g->rb_grid), block(kRemThreads);
-  if (epi == EPI_BWD) return launch_rem<EPI_BWD>(grid, block, lds, s, a, L);
-  return launch_rem<EPI_FWD>(grid, block, lds, s, a, L);
+  if (epi == EPI_BWD)
+    return vf ? launch_rem<EPI_BWD, true>(grid, block, lds, s, a, L)
+              : launch_rem<EPI_BWD, false>(grid, block, lds, s, a, L);
+  return vf ? launch_rem<EPI_FWD, true>(grid, block, lds, s, a, L)
+            : launch_rem<EPI_FWD, false>(grid, block, lds, s, a, L);
 }
 
 hipError_t launch_split_copy(const float* h, int64_t ld_h, int64_t n, int64_t f, int64_t fs,
-                             float* main, float* rem, hipStream_t s) {
+                             float* main, float* rem, const float* rem_scale, hipStream_t s) {
   const int64_t total = n * (fs / 4 + 1);
   if (total <= 0) return hipSuccess;
   const int64_t blocks = std::min<int64_t>((total + kBlock - 1) / kBlock, 1 << 20);
   hipLaunchKernelGGL(k_split_copy, dim3((unsigned)blocks), dim3(kBlock), 0, s, h, ld_h, n,
-                     (int)f, (int)fs, main, rem);
+                     (int)f, (int)fs, main, rem, rem_scale);
   return hipGetLastError();
 }
 

@@ -117,7 +117,8 @@ int propagate_split(const appnp_graph* g, const StepArgs& a0, const void* H, int
   auto rem_of = [&](int i) { return reinterpret_cast<float*>(bufs[i] + main_b); };
   const float* h = static_cast<const float*>(H);
   float* z = static_cast<float*>(Z);
-  int rc = dev_err(appnp::launch_split_copy(h, ld_h, n, f, fs, main_of(0), rem_of(0), s));
+  int rc = dev_err(appnp::launch_split_copy(h, ld_h, n, f, fs, main_of(0), rem_of(0),
+                                            appnp::remainder_scale(g), s));
   StepArgs am = a0, ar = a0;  // main / remainder chain
   am.f = (int32_t)fs;
   am.h = H;
@@ -136,7 +137,7 @@ int propagate_split(const appnp_graph* g, const StepArgs& a0, const void* H, int
     set_drop(ar, p_drop, seed, k);
     rc = dev_err(appnp::launch_remainder(g, ar, appnp::EPI_FWD, rem_of(cur), h + fs, ld_h,
                                          last ? z + fs : rem_of(dst), last ? ld_z : 4,
-                                         last ? (int)(f - fs) : 4, s));
+                                         last ? (int)(f - fs) : 4, !last, s));
     cur = dst;
   }
   return rc;
@@ -154,7 +155,8 @@ int propagate_bwd_split(const appnp_graph* g, const StepArgs& a0, const void* dZ
   auto main_of = [&](int i) { return reinterpret_cast<float*>(bufs[i]); };
   auto rem_of = [&](int i) { return reinterpret_cast<float*>(bufs[i] + main_b); };
   int rc = dev_err(appnp::launch_split_copy(static_cast<const float*>(dZ), ld_dz, n, f, fs,
-                                            main_of(0), rem_of(0), s));
+                                            main_of(0), rem_of(0), appnp::remainder_scale(g),
+                                            s));
   StepArgs am = a0, ar = a0;  // main / remainder chain
   am.f = (int32_t)fs;
   am.aux = dH;
@@ -175,7 +177,8 @@ int propagate_bwd_split(const appnp_graph* g, const StepArgs& a0, const void* dZ
     set_drop(ar, p_drop, seed, k);
     ar.alpha = a_k;
     rc = dev_err(appnp::launch_remainder(g, ar, appnp::EPI_BWD, rem_of(cur), dh_rem, ld_dh,
-                                         k == 0 ? nullptr : rem_of(dst), 4, (int)(f - fs), s));
+                                         k == 0 ? nullptr : rem_of(dst), 4, (int)(f - fs), true,
+                                         s));
     cur = dst;
   }
   return rc;
@@ -305,8 +308,9 @@ int appnp_graph_source_blocks(const appnp_graph* g, int64_t* bytes) {
   if (!g || !bytes) return APPNP_EINVAL;
   *bytes = 0;
   if (g->rb_off)
-    *bytes = g->rb_total * 8 + g->rb_total / 16 +
-             ((int64_t)g->rb_passes * g->rb_nb * g->rb_slots + 1) * (int64_t)sizeof(int32_t);
+    *bytes = g->rb_total * (g->rb_val ? 8 : 4) + g->rb_total / 16 +
+             ((int64_t)g->rb_passes * g->rb_nb * g->rb_slots + 1) * (int64_t)sizeof(int32_t) +
+             (g->rb_dl ? g->n * 4 : 0) + (g->rb_dr ? g->n * 4 : 0);
   return APPNP_OK;
 }
 

@@ -68,12 +68,15 @@ __global__ __launch_bounds__(kBlock) void k_degree(const int32_t* __restrict__ i
   if (i >= n) return;
   double s = 0.0;
   int32_t c_all = 0, c_loc = 0, c_rem = 0;
+  bool unit = true;
   walk_merged_row(indptr, indices, vals, i, n, err, [&](int32_t j, double a) {
     s += a;
+    unit = unit && a == 1.0;
     ++c_all;
     if (j >= row_lo && j < row_hi) ++c_loc; else ++c_rem;
   });
   dinv[i] = mode == APPNP_NORM_SYM ? 1.0 / sqrt(s) : 1.0 / s;
+  if (!unit) atomicOr(err + 2, 1u);  // some entry of A+I is not 1 (flags[2])
   if (i >= row_lo && i < row_hi) {
     const int64_t r = i - row_lo;
     cnt.all[r] = c_all;
@@ -312,7 +315,8 @@ void graph_free(appnp_graph* g) {
   if (!g) return;
   void* ptrs[] = {g->row_ptr, g->col, g->val, g->lrow_ptr, g->lcol, g->lval,
                   g->rrow_ptr, g->rcol, g->rval, g->dinv, g->t_row_ptr, g->t_col, g->t_val,
-                  g->heavy, g->t_heavy, g->hub, g->t_hub, g->rb_off, g->rb_ent, g->rb_val, g->rb_cblk};
+                  g->heavy, g->t_heavy, g->hub, g->t_hub, g->rb_off, g->rb_ent, g->rb_val, g->rb_cblk,
+                  g->rb_dl, g->rb_dr};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   g->row_ptr = g->col = g->lrow_ptr = g->lcol = g->rrow_ptr = g->rcol = nullptr;
@@ -325,6 +329,7 @@ void graph_free(appnp_graph* g) {
   g->rb_ent = nullptr;
   g->rb_val = nullptr;
   g->rb_cblk = nullptr;
+  g->rb_dl = g->rb_dr = nullptr;
   g->rb_nb = g->rb_passes = 0;
   g->rb_total = 0;
 }
@@ -347,9 +352,9 @@ int graph_build(const int32_t* indptr, const int32_t* indices, const float* vals
   int32_t *cnt = nullptr, *cnt_l = nullptr, *cnt_r = nullptr;
   int64_t* bsum = nullptr;
   int64_t* totals = nullptr;  // [3]
-  unsigned* flags = nullptr;  // [2]: err, asym
+  unsigned* flags = nullptr;  // [3]: err, asym, non-unit weights
   int64_t h_tot[3] = {0, 0, 0};
-  unsigned h_flags[2] = {0, 0};
+  unsigned h_flags[3] = {0, 0, 0};
   const int64_t nb_scan = std::max<int64_t>(1, (rows + kScanTile - 1) / kScanTile);
   const unsigned blocks_n = (unsigned)std::max<int64_t>(1, (n + kBlock - 1) / kBlock);
   const unsigned blocks_r = (unsigned)std::max<int64_t>(1, (rows + kBlock - 1) / kBlock);
@@ -373,8 +378,8 @@ int graph_build(const int32_t* indptr, const int32_t* indices, const float* vals
   }
   APPNP_TRY(dalloc(&bsum, nb_scan));
   APPNP_TRY(dalloc(&totals, 3));
-  APPNP_TRY(dalloc(&flags, 2));
-  APPNP_TRY(hipMemsetAsync(flags, 0, 2 * sizeof(unsigned), s));
+  APPNP_TRY(dalloc(&flags, 3));
+  APPNP_TRY(hipMemsetAsync(flags, 0, 3 * sizeof(unsigned), s));
   APPNP_TRY(hipMemsetAsync(totals, 0, 3 * sizeof(int64_t), s));
 
   rc_ptrs = RowCounts{cnt, cnt_l, cnt_r};
@@ -403,6 +408,7 @@ int graph_build(const int32_t* indptr, const int32_t* indices, const float* vals
     goto done;
   }
   g->symmetric = h_flags[1] == 0 ? 1 : 0;
+  g->unit = h_flags[2] == 0 ? 1 : 0;
   g->nnz_hat = h_tot[0];
   g->nnz_local = h_tot[1];
   g->nnz_remote = h_tot[2];

@@ -15,6 +15,8 @@ struct appnp_graph {
   int64_t nnz_local = 0, nnz_remote = 0;
   int mode = 0;          // APPNP_NORM_SYM / APPNP_NORM_RW
   int symmetric = 0;     // A's pattern and weights are symmetric
+  int unit = 0;          // every entry of A+I is 1 (unweighted A, no self loops): A_hat is
+                         // dl_i * dr_j with per-row scales (sym: dinv, dinv; rw: dinv, 1)
   int split = 0;         // local/remote CSRs present
   int device = 0;
   int32_t* row_ptr = nullptr;   // [rows+1]
@@ -43,7 +45,9 @@ struct appnp_graph {
   // rows whose column lies in that block, sorted by (row, column), padded to 64 entries
   int32_t* rb_off = nullptr;    // [rb_passes * rb_slots * rb_nb + 1] segment starts
   uint32_t* rb_ent = nullptr;   // [rb_total] (row in group << kRemColBits) | column in block
-  float* rb_val = nullptr;      // [rb_total]
+  float* rb_val = nullptr;      // [rb_total]; null for a unit graph (values from rb_dl/rb_dr)
+  float* rb_dl = nullptr;       // unit graph: [n] fp32 dinv, the row scale of A_hat
+  float* rb_dr = nullptr;       // unit graph, sym: [n] fp32 dinv, the column scale (rw: null)
   int32_t* rb_cblk = nullptr;   // [rb_total / 64] source block of each chunk of 64 entries
   int64_t rb_total = 0;         // entries including the padding
   int32_t rb_nb = 0;            // source blocks of 2^rb_br_log2 rows
@@ -78,11 +82,17 @@ hipError_t exclusive_scan(const int32_t* cnt, int64_t rows, int32_t* out, int64_
 
 // appnp_blocks.hip
 int graph_build_source_blocks(appnp_graph* g, hipStream_t s);
+// to_rem: out is the next remainder buffer (a unit graph stores dr o y there), not Z / dH
 hipError_t launch_remainder(const appnp_graph* g, const StepArgs& a, int epi,
                             const float* z_rem, const float* h_rem, int64_t ld_h, float* out,
-                            int64_t ld_out, int nv, hipStream_t s);
+                            int64_t ld_out, int nv, bool to_rem, hipStream_t s);
+// rem_scale (nullable): per-row factor of the remainder part (remainder_scale(g))
 hipError_t launch_split_copy(const float* h, int64_t ld_h, int64_t n, int64_t f, int64_t fs,
-                             float* main, float* rem, hipStream_t s);
+                             float* main, float* rem, const float* rem_scale, hipStream_t s);
+// the factor the remainder buffers carry: dr for a value-free (unit) layout, else none
+inline const float* remainder_scale(const appnp_graph* g) {
+  return g->rb_val ? nullptr : g->rb_dr;
+}
 
 // appnp_spmm.hip
 int pick_vec(int dtype, int64_t f, const int64_t* lds, int n_ld, const void* const* ptrs,
