@@ -61,7 +61,10 @@ constexpr uint32_t kRemNone = 0xffffffffu;      // packed entry of an idle lane 
 constexpr int kWalkWaves = kWavesPerBlock;      // build walk: one wave per group
 constexpr int kWalkMaxBlocks = 4096;            // LDS cursors of the build walk: 64 KiB
 constexpr int kRemChunk = kWave;                // entries per chunk; segments padded to it
-constexpr int kRemU = 8;                        // chunks in flight per wave
+#ifndef APPNP_REM_U
+#define APPNP_REM_U 2
+#endif
+constexpr int kRemU = APPNP_REM_U;              // chunks in flight per wave (-DAPPNP_REM_U: measurement)
 
 static_assert(kRemMaxRg < (1 << kRemRowBits), "row in group must fit the packed entry");
 static_assert(kRemRowBits + kRemColBits == 32, "packed entry is 32 bits");
@@ -87,17 +90,20 @@ constexpr int kDppRowShr1 = 0x111, kDppRowShr2 = 0x112, kDppRowShr4 = 0x114,
               kDppRowShr8 = 0x118, kDppRowBcast15 = 0x142, kDppRowBcast31 = 0x143,
               kDppWaveShr1 = 0x138;  // whole-wave shift by one lane (GFX9 family)
 
+// bound_ctrl: a lane whose source lane is out of its row (or outside ROW_MASK's rows) reads 0
+// for both the row and the partial.  A spurious match on row 0 then adds 0.0, so no 'old'
+// operand needs initialising (five fewer moves per step).
 template <int CTRL, int ROW_MASK>
 __device__ __forceinline__ void seg_step(int row, f32x4& v) {
-  const int src_row = __builtin_amdgcn_update_dpp(-1, row, CTRL, ROW_MASK, 0xf, false);
+  const int src_row = __builtin_amdgcn_update_dpp(0, row, CTRL, ROW_MASK, 0xf, true);
   const float ux = __int_as_float(
-      __builtin_amdgcn_update_dpp(0, __float_as_int(v.x), CTRL, ROW_MASK, 0xf, false));
+      __builtin_amdgcn_update_dpp(0, __float_as_int(v.x), CTRL, ROW_MASK, 0xf, true));
   const float uy = __int_as_float(
-      __builtin_amdgcn_update_dpp(0, __float_as_int(v.y), CTRL, ROW_MASK, 0xf, false));
+      __builtin_amdgcn_update_dpp(0, __float_as_int(v.y), CTRL, ROW_MASK, 0xf, true));
   const float uz = __int_as_float(
-      __builtin_amdgcn_update_dpp(0, __float_as_int(v.z), CTRL, ROW_MASK, 0xf, false));
+      __builtin_amdgcn_update_dpp(0, __float_as_int(v.z), CTRL, ROW_MASK, 0xf, true));
   const float uw = __int_as_float(
-      __builtin_amdgcn_update_dpp(0, __float_as_int(v.w), CTRL, ROW_MASK, 0xf, false));
+      __builtin_amdgcn_update_dpp(0, __float_as_int(v.w), CTRL, ROW_MASK, 0xf, true));
   if (src_row == row) {
     v.x += ux;
     v.y += uy;

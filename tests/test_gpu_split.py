@@ -111,7 +111,7 @@ def test_split_padded_views_and_determinism(graphs, ahat):
 
 
 def test_split_backward_and_training_path(graphs, ahat):
-    """The adjoint stays on the whole-row path; the autograd op composes both."""
+    """The autograd op composes the split forward and the split adjoint."""
     import ppnp_amd
 
     f = 100
@@ -172,6 +172,37 @@ def test_split_weighted_and_rw(adj, mode):
     Z = ppnp_amd.propagate_forward(G, H.to(DEV), 3, 0.15, p_drop=0.2, seed=5)
     ref = O.appnp_propagate(O.calc_a_hat(w, mode), H.numpy(), 3, 0.15, p_drop=0.2, seed=5)
     close_fp32(Z.double().cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("case", ["unit-rw", "self-loops"])
+def test_split_value_free_layout(adj, case):
+    """A unit graph (every entry of A+I is 1) stores no values in the source-blocked copy: the
+    remainder buffers carry dr o Z and the epilogue scales by dl (sym: dinv both sides, rw:
+    dinv and 1).  'rw' exercises dr = 1; self loops in an unweighted A make the diagonal of
+    A+I equal 2, so that graph must keep its values -- same parity either way."""
+    import ppnp_amd
+
+    mode = "rw" if case == "unit-rw" else "sym"
+    a = adj
+    if case == "self-loops":
+        a = (adj + sp.diags(np.r_[np.ones(1000), np.zeros(N - 1000)].astype(np.float32))).tocsr()
+        a.eliminate_zeros()
+        a.sort_indices()
+    G = ppnp_amd.Graph.from_scipy(a, mode=mode, device=DEV, features=100)
+    assert G.split_point(100) == 96
+    w = adj.copy()
+    w.data = np.full(w.nnz, 2.0, dtype=np.float32)  # weighted twin: same pattern, with values
+    Gw = ppnp_amd.Graph.from_scipy(w, mode=mode, device=DEV, features=100)
+    if case == "unit-rw":
+        assert G.source_block_bytes() < Gw.source_block_bytes()  # no value stream
+    else:
+        assert G.source_block_bytes() >= Gw.source_block_bytes()  # values kept
+    H = _h(100, 15)
+    Z = ppnp_amd.propagate_forward(G, H.to(DEV), 3, 0.15, p_drop=0.2, seed=9)
+    ref = O.appnp_propagate(O.calc_a_hat(a, mode), H.numpy(), 3, 0.15, p_drop=0.2, seed=9)
+    close_fp32(Z.double().cpu().numpy(), ref)
+    Z = ppnp_amd.propagate_forward(G, H.to(DEV), 4, 0.1)
+    close_fp32(Z.double().cpu().numpy(), O.appnp_propagate(O.calc_a_hat(a, mode), H.numpy(), 4, 0.1))
 
 
 def test_split_exact_size_last_row(graphs, ahat):
