@@ -63,8 +63,9 @@ enum appnp_norm { APPNP_NORM_SYM = 0, APPNP_NORM_RW = 1 };
  * block; full graphs only).  appnp_propagate then takes the last 1-4 columns of fp32 rows
  * with F = 32q + r (e.g. F = 100) out of the random gather and forms their product in one
  * persistent, L2-resident pass per iteration, so a gathered row costs q cache lines instead
- * of q + 1.  Costs 8 bytes per nonzero plus one int32 per (block, 640-row group) of device
- * memory (segments padded to 64 entries).  Best-effort: when the copy cannot be built (too many blocks, device memory), the
+ * of q + 1.  Costs 8 bytes per nonzero (4 on an unweighted graph without self loops, whose
+ * entries need no values, plus 8 bytes per node) plus one int32 per (block, 640-row group) of
+ * device memory (segments padded to 64 entries).  Best-effort: when the copy cannot be built (too many blocks, device memory), the
  * graph is still created and gathers whole rows; appnp_graph_source_blocks tells. */
 #define APPNP_GRAPH_SOURCE_BLOCKS 0x200
 
