@@ -10,7 +10,8 @@ compares the WHOLE Z_K with an oracle computed on the CPU from the same A and H:
   <= 2e-2 max|Z_ref| with >= 98 % argmax agreement (DESIGN.md 2);
 * config 5, products-synth (2,449,029 x 100, K = 10, fp32; 126 M nonzeros): the split-row path
   (96 gathered columns + the L2-blocked remainder pass) against a float64 torch.sparse CPU
-  loop over the same A_hat, all ten iterations;
+  loop over the same A_hat, all ten iterations -- forward, the adjoint, and the power-law
+  graph of the same size (hub rows);
 * config 4 row-partitioned over 2 and 4 ranks sharing the one GPU (gloo exchange, with and
   without the overlapped local/remote split), each rank against the float64 oracle:
   tests/dist_worker.py launched by torch.distributed.run as fresh child processes.
@@ -84,25 +85,69 @@ def test_config3_msacad_bf16_full_size():
     assert (got.argmax(1) == ref.argmax(1)).mean() >= 0.98
 
 
-def test_products_k10_matches_oracle():
-    """Config 5 at full size, K = 10, on the split-row path -- every one of the 244.9 M values."""
+def _products_case(name):
+    """The full-size split-path case of workload ``name``: its graph (built with the bench's
+    source-blocked copy), H, and A_hat as a float64 torch.sparse CSR on the CPU."""
     import ppnp_amd
 
-    n, F, K, alpha, dtype, indptr, indices, H = _workload("products-synth")
+    n, F, K, alpha, dtype, indptr, indices, H = _workload(name)
     G = ppnp_amd.Graph.from_csr(indptr, indices, None, n, device=DEV, features=F, dtype=dtype)
     assert G.split_point(F) == 96  # the bench's path: 3 gathered lines + remainder pass
-    Z = ppnp_amd.propagate_forward(G, H, K, alpha).cpu()
     rp, col, val, _ = G.csr()
-    del indices, G
     a = torch.sparse_csr_tensor(rp.cpu().long(), col.cpu().long(), val.cpu().double(),
                                 size=(n, n))
-    del rp, col, val
+    del rp, col, val, indices
     torch.set_num_threads(max(1, min(16, len(os.sched_getaffinity(0)))))
-    Hc = H.cpu().double()
-    ref = O.appnp_propagate_torch_cpu(a, Hc, K, alpha)  # float64 operator and iterates
-    err = float((Z.double() - ref).abs().max())
+    return G, H, K, alpha, a
+
+
+def _check_full(got, ref):
+    err = float((got.double() - ref).abs().max())
     tol = 1e-5 * float(ref.abs().max()) + 1e-6
     assert err <= tol, (err, tol)
+
+
+@pytest.fixture(scope="module")
+def products():
+    G, H, K, alpha, a = _products_case("products-synth")
+    yield G, H, K, alpha, a
+    G.close()
+
+
+def test_products_k10_matches_oracle(products):
+    """Config 5 at full size, K = 10, on the split-row path -- every one of the 244.9 M values
+    against the float64 torch.sparse CPU loop of the same A_hat (helpers.py:58-66)."""
+    import ppnp_amd
+
+    G, H, K, alpha, a = products
+    Z = ppnp_amd.propagate_forward(G, H, K, alpha).cpu()
+    _check_full(Z, O.appnp_propagate_torch_cpu(a, H.cpu().double(), K, alpha))
+
+
+def test_products_k10_backward_matches_oracle(products):
+    """The adjoint at full size on the split path (appnp_propagate_bwd: main-column chain plus
+    the remainder pass with its adjoint epilogue).  Without dropout APPNP_K is a polynomial in
+    the symmetric A_hat, so J^T dZ = APPNP_K(dZ): the float64 forward loop is its oracle."""
+    import ppnp_amd
+
+    G, H, K, alpha, a = products
+    g = torch.Generator(device="cpu").manual_seed(11)
+    dZ = torch.randn(H.shape, generator=g, dtype=torch.float32)
+    dH = ppnp_amd.propagate_backward(G, dZ.to(DEV), K, alpha).cpu()
+    _check_full(dH, O.appnp_propagate_torch_cpu(a, dZ.double(), K, alpha))
+
+
+def test_products_powerlaw_k10_matches_oracle():
+    """The Chung-Lu power-law graph with products' node and edge counts (hub rows: the heavy /
+    hub lists of the main SpMM and long runs in the remainder pass) at full size, K = 10."""
+    import ppnp_amd
+
+    G, H, K, alpha, a = _products_case("products-powerlaw")
+    try:
+        Z = ppnp_amd.propagate_forward(G, H, K, alpha).cpu()
+    finally:
+        G.close()
+    _check_full(Z, O.appnp_propagate_torch_cpu(a, H.cpu().double(), K, alpha))
 
 
 def _free_port():
