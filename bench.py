@@ -45,7 +45,7 @@ GATHER_LINE_CEILING = 56.0
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--steps", type=int, default=20)  # median of >= 20 after 3 warm-ups
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--workload", default="products-synth")
     p.add_argument("--dtype", default=None, choices=["f32", "bf16"],
