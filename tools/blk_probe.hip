@@ -2,7 +2,7 @@
 // (k_rem_persist, 16-B rows) widened to W = 4 * LPE fp32 columns.  Not part of the library.
 //
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 tools/blk_probe.hip -o tools/bin/blk_probe
-//   tools/bin/blk_probe W:br:U [W:br:U ...]      (W in 4, 8, 16, 32; br = log2 source rows
+//   [BLK_N=n BLK_DEG=d] tools/bin/blk_probe W:br:U [W:br:U ...]   (W in 4, 8, 16, 32; br = log2 source rows
 //                                                 per block; U = chunks in flight per wave)
 //
 // Question: the random-gather SpMM is bound by ~56 G line requests/s from
@@ -269,7 +269,9 @@ float run_blk(const Graph& G, int br, const f4* d_z, f4* d_y, float w, hipEvent_
 
 int main(int argc, char** argv) {
   Graph G;
-  const int n = 2449029, deg = 51;
+  // BLK_N / BLK_DEG: another graph shape (arxiv-synth: BLK_N=169343 BLK_DEG=14)
+  const int n = getenv("BLK_N") ? atoi(getenv("BLK_N")) : 2449029;
+  const int deg = getenv("BLK_DEG") ? atoi(getenv("BLK_DEG")) : 51;
   G.n = n;
   G.nnz = (int64_t)n * (deg + 1);
   const float w = 1.0f / (deg + 1);
@@ -308,7 +310,7 @@ int main(int argc, char** argv) {
   CHECK(hipEventCreate(&b));
   int cus = 0;
   CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
-  printf("# one W-column fp32 slab of products-synth's shape: n = %d, nnz = %lld, %d CUs\n", n,
+  printf("# one W-column fp32 slab: n = %d, %d uniform columns + the diagonal per row, nnz = %lld, %d CUs\n", n, deg,
          (long long)G.nnz, cus);
   printf("variant      W  block_rows  U  ms_per_pass  G_nonzeros_per_s  padding  max|diff|\n");
   std::vector<float> y0, y1;
