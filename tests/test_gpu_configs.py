@@ -137,6 +137,20 @@ def test_products_k10_backward_matches_oracle(products):
     _check_full(dH, O.appnp_propagate_torch_cpu(a, dZ.double(), K, alpha))
 
 
+def test_products_k10_bf16_matches_oracle(products):
+    """bf16 storage with fp32 accumulation at products scale (whole 200-B rows: the split path
+    is fp32-only), against the float64 loop on the bf16-rounded H: the bf16 bar of DESIGN.md 2."""
+    import ppnp_amd
+
+    G, H, K, alpha, a = products
+    Hb = H.to(torch.bfloat16)
+    assert G.split_point(int(H.shape[1]), torch.bfloat16) == 0
+    Z = ppnp_amd.propagate_forward(G, Hb, K, alpha).float().cpu().double()
+    ref = O.appnp_propagate_torch_cpu(a, Hb.float().cpu().double(), K, alpha)
+    assert float((Z - ref).abs().max()) <= 2e-2 * float(ref.abs().max())
+    assert float((Z.argmax(1) == ref.argmax(1)).double().mean()) >= 0.98
+
+
 def test_products_powerlaw_k10_matches_oracle():
     """The Chung-Lu power-law graph with products' node and edge counts (hub rows: the heavy /
     hub lists of the main SpMM and long runs in the remainder pass) at full size, K = 10."""
