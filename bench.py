@@ -270,6 +270,12 @@ def main():
     if world > 1 and torch.distributed.get_backend() == "nccl":
         ctl = torch.distributed.new_group(backend="gloo")
 
+    stagger = float(os.environ.get("PPNP_BENCH_STAGGER") or 0)
+    if stagger and world > 1:
+        # rehearsals with all ranks on ONE GPU only: concurrent generation of a products-sized
+        # graph by 8 processes time-slicing one device stalls in torch.unique for minutes
+        # (0.23 s alone), so rank r starts r * stagger seconds late; never set on a real node
+        time.sleep(rank * stagger)
     t0 = time.perf_counter()
     indptr, indices = synth.graph_for(args.workload, device=dev)
     H = synth.features(n, F, dtype=dtype, device=dev)
@@ -280,6 +286,8 @@ def main():
         H = Hbuf[:, :F]
     torch.cuda.synchronize()
     t_gen = time.perf_counter() - t0
+    if rank == 0 and world > 1:
+        log(f"[bench] {args.workload}: graph and H generated in {t_gen:.2f}s")
 
     autotune = None
     if distributed:
