@@ -413,9 +413,10 @@ def main():
     # L2-blocked remainder pass (appnp_blocks.hip)
     # (single GPU, or a column layout, whose ranks call appnp_propagate on their slab)
     whole = not distributed or runner.layout.rows == 1
-    fs = graph.split_point(F_local, dtype) if whole and K >= 2 else 0
+    r_cols = graph.remainder_cols(F_local, dtype) if whole and K >= 2 else 0
+    fs = F_local - r_cols if r_cols else 0
     ld_l = pdist.line_ld(F_local, s)
-    lines_per_row = (fs * s // 128 if fs else
+    lines_per_row = (fs * s // 128 if r_cols else
                      1 if ld_l * s <= 128 else -(-(F_local * s) // 128))
     lines = nnz_local * lines_per_row + (8 * nnz_local + 3 * rows_local * ld_l * s) / 128
     line_rate = lines / (avg_launch_ms * 1e-3) / 1e9
@@ -476,7 +477,9 @@ def main():
                 "frac": line_rate / GATHER_LINE_CEILING,
                 "ceiling_source": "tools/gather_probe.hip, profiles/r1_gather_probe.txt",
             },
-            "kernel": ("k_step_wide (one launch per iteration)" if not fs else
+            "kernel": ("k_step_wide (one launch per iteration)" if not r_cols else
+                       ("k_rem_persist on all the slab's columns (narrow rows: one persistent "
+                        "L2-blocked launch per iteration)") if not fs else
                        f"k_step_wide on columns [0, {fs}) of the slab + k_rem_persist (the "
                        f"remainder columns, one persistent L2-blocked launch) per iteration; "
                        f"times are per iteration"),

@@ -26,6 +26,8 @@ APPNP_ENOTSUP = -95
 NORM = {"sym": 0, "rw": 1}
 GRAPH_TRANSPOSE = 0x100
 GRAPH_SOURCE_BLOCKS = 0x200
+GRAPH_SB_W8 = 0x400  # remainder of up to 8 columns (include/ppnp_amd.h)
+GRAPH_SB_W16 = 0x800  # up to 16
 F32, BF16 = 0, 1
 PART_ALL, PART_LOCAL, PART_REMOTE = 0, 1, 2
 
@@ -50,6 +52,7 @@ _SIGS = {
     "appnp_graph_dinv": (_i32, [_vp, C.POINTER(_vp)]),
     "appnp_workspace_bytes": (_sz, [_vp, _i64, _i64, _i32]),
     "appnp_propagate_split_point": (_i32, [_vp, _i64, _i32, C.POINTER(_i64)]),
+    "appnp_propagate_remainder_cols": (_i32, [_vp, _i64, _i32, C.POINTER(_i64)]),
     "appnp_graph_source_blocks": (_i32, [_vp, C.POINTER(_i64)]),
     "appnp_propagate": (
         _i32,

@@ -45,6 +45,14 @@
 // dl_i dr_j with sym: dl = dr = dinv, rw: dl = dinv, dr = 1) stores NO values: the remainder
 // buffers hold dr o Z_rem, the pass sums the gathered rows and the epilogue scales by dl_i.
 // The entry stream halves (4 B per entry): 0.91 -> 0.81 ms per products-synth launch.
+//
+// Wider remainders (APPNP_GRAPH_SB_W8 / APPNP_GRAPH_SB_W16): the same pass over rows of
+// W = 4 LPE fp32 columns, LPE = 2 or 4 lanes per entry, laid out piece-major (lane = piece * CH +
+// entry, CH = 64 / LPE entries per chunk), so every 16-lane DPP row holds one 16-B piece of up to
+// 16 consecutive entries and the segmented scan compares (row, piece).  A wave group holds
+// 640 / LPE rows.  It takes 5-16 remainder columns (F = 32q + r) and narrow rows (F <= W) out
+// of the random gather (tools/blk_probe.hip: 16 columns of products' shape 1.89 against 2.38 ms
+// per pass).  LPE = 1 is the pass above, unchanged.
 #include <algorithm>
 #include <cstdlib>
 
@@ -120,6 +128,7 @@ __device__ __forceinline__ void seg_step(int row, f32x4& v) {
 // (bcast31) continues a run.  So the result is the full six-step scan's, bit for bit.  Runs in
 // a chunk are short (a group's row has ~0.7 entries per source block), so most chunks need
 // two or three steps.
+template <int CH>
 __device__ __forceinline__ void seg_scan(int row, f32x4& v, unsigned long long heads) {
   unsigned long long m = ~(heads | 0x0001000100010001ull);  // lanes >= 1 after their head
   if (m) {
@@ -134,9 +143,14 @@ __device__ __forceinline__ void seg_scan(int row, f32x4& v, unsigned long long h
       }
     }
   }
-  if (~heads & ((1ull << 16) | (1ull << 48)))
-    seg_step<kDppRowBcast15, 0xa>(row, v);  // rows 1, 3 <- lanes 15, 47
-  if (~heads & (1ull << 32)) seg_step<kDppRowBcast31, 0xc>(row, v);  // rows 2, 3 <- lane 31
+  // runs cross 16-lane rows only where a piece spans several of them (CH = 32, 64)
+  if constexpr (CH >= 32) {
+    if (~heads & ((1ull << 16) | (1ull << 48)))
+      seg_step<kDppRowBcast15, 0xa>(row, v);  // rows 1, 3 <- lanes 15, 47
+  }
+  if constexpr (CH == 64) {
+    if (~heads & (1ull << 32)) seg_step<kDppRowBcast31, 0xc>(row, v);  // rows 2, 3 <- lane 31
+  }
 }
 
 // Epilogue of one row of the iteration: FWD out[i, :nv] = (1-alpha) R[i] + alpha H_rem[i]
@@ -192,17 +206,53 @@ __device__ __forceinline__ void rem_finish(const StepArgs& a, const RemLayout& L
   }
 }
 
+// The epilogue of piece q (columns 4q .. 4q+3 of the remainder) of one row for LPE > 1.
+// a.f = nv: the valid remainder columns (f - fs), on every iteration; L.scale_out: the output
+// is the next remainder buffer (rows of 4 LPE floats, a.ld_out = 4 LPE; unit graph: dr o y)
+// rather than Z (only the valid columns).  FWD reads H_rem's valid columns only; BWD adds
+// alpha' G_k into dH's valid columns.
+template <int EPI, bool VF, int LPE>
+__device__ __forceinline__ void rem_finish_piece(const StepArgs& a, const RemLayout& L, int64_t i,
+                                                 int q, f32x4 acc) {
+  const int nv = a.f - 4 * q;  // valid columns of this piece (may be <= 0)
+  float so = 1.0f;
+  if constexpr (VF) {
+    const float dl = L.dl[i];
+    acc = f32x4{dl * acc.x, dl * acc.y, dl * acc.z, dl * acc.w};
+    if (L.scale_out && L.dr) so = L.dr[i];
+  }
+  float y[4] = {a.scale * acc.x, a.scale * acc.y, a.scale * acc.z, a.scale * acc.w};
+  if constexpr (EPI == EPI_BWD) {
+    if (a.out)
+      static_cast<f32x4*>(a.out)[i * LPE + q] = f32x4{so * y[0], so * y[1], so * y[2], so * y[3]};
+    float* d = a.rem_dh + i * a.ld_rem_dh + 4 * q;
+    for (int v = 0; v < 4 && v < nv; ++v) d[v] = fmaf(a.alpha, y[v], d[v]);
+  } else {
+    const float* hp = static_cast<const float*>(a.h) + i * a.ld_h + 4 * q;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) y[v] = v < nv ? fmaf(a.alpha, hp[v], y[v]) : y[v];
+    if (L.scale_out) {
+      static_cast<f32x4*>(a.out)[i * LPE + q] = f32x4{so * y[0], so * y[1], so * y[2], so * y[3]};
+    } else {
+      float* o = static_cast<float*>(a.out) + i * a.ld_out + 4 * q;
+      for (int v = 0; v < 4 && v < nv; ++v) o[v] = y[v];
+    }
+  }
+}
+
 // One iteration of the remainder columns over all source blocks (see the file comment).
 // a.zin = Z_rem (n x 4 fp32; VF: dr o Z_rem); U chunks of 64 entries in flight per wave.
 // VF (unit graph): entries carry no value -- the sum of the gathered dr_j Z_j is scaled by
 // dl_i in the epilogue, so the entry stream is 4 B per entry instead of 8 (0.91 -> 0.81 ms
 // per products-synth launch).
-template <int EPI, int U, bool VF>
+template <int EPI, int U, bool VF, int LPE>
 __global__ __launch_bounds__(kRemThreads) void k_rem_persist(StepArgs a, RemLayout L) {
+  constexpr int CH = kWave / LPE;  // entries per chunk; piece q of entry e on lane q * CH + e
   extern __shared__ f32x4 rem_acc[];
   const int lane = threadIdx.x & (kWave - 1);
+  const int q = lane / CH, le = lane % CH;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  f32x4* acc = rem_acc + (int64_t)wv * L.rg;
+  f32x4* acc = rem_acc + (int64_t)wv * L.rg * LPE;
   const f32x4* __restrict__ z = static_cast<const f32x4*>(a.zin);
   const int64_t slot = (int64_t)blockIdx.x * kRemWaves + wv;
   const uint32_t cmask = (1u << kRemColBits) - 1u;
@@ -210,11 +260,11 @@ __global__ __launch_bounds__(kRemThreads) void k_rem_persist(StepArgs a, RemLayo
     const int64_t g = (int64_t)p * L.slots + slot;
     const int64_t r0 = g * L.rg;
     const int rows = (int)max<int64_t>(0, min<int64_t>(L.rg, a.n_rows - r0));
-    for (int r = lane; r < rows; r += kWave) acc[r] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    for (int r = lane; r < rows * LPE; r += kWave) acc[r] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     // this wave's stream: blocks 0..nb-1 back to back, each a whole number of chunks; the
     // block of chunk c is cblk[c]
-    const int32_t c_end = L.off[(g + 1) * L.nb] / kRemChunk;
-    for (int32_t c = L.off[g * L.nb] / kRemChunk; c < c_end; c += U) {
+    const int32_t c_end = L.off[(g + 1) * L.nb] / CH;
+    for (int32_t c = L.off[g * L.nb] / CH; c < c_end; c += U) {
       const int nch = min(U, c_end - c);
       int32_t cb[U];  // first source row of each chunk's block (wave-uniform: scalar loads)
       uint32_t en[U];
@@ -225,7 +275,7 @@ __global__ __launch_bounds__(kRemThreads) void k_rem_persist(StepArgs a, RemLayo
         en[u] = kRemNone;
         wt[u] = 1.0f;
         if (u < nch) {
-          const int64_t e = (int64_t)(c + u) * kRemChunk + lane;
+          const int64_t e = (int64_t)(c + u) * CH + le;
           cb[u] = L.cblk[c + u] << L.br_log2;
           en[u] = ld_nt<uint32_t>(L.ent + e);
           if constexpr (!VF) wt[u] = ld_nt<float>(L.val + e);
@@ -233,14 +283,22 @@ __global__ __launch_bounds__(kRemThreads) void k_rem_persist(StepArgs a, RemLayo
       }
       f32x4 zv[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u)
-        zv[u] = en[u] != kRemNone ? z[cb[u] + (int32_t)(en[u] & cmask)]
-                                  : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+      for (int u = 0; u < U; ++u) {
+        if constexpr (LPE == 1) {
+          zv[u] = en[u] != kRemNone ? z[cb[u] + (int32_t)(en[u] & cmask)]
+                                    : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        } else {
+          zv[u] = en[u] != kRemNone ? z[(int64_t)(cb[u] + (int32_t)(en[u] & cmask)) * LPE + q]
+                                    : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        }
+      }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if (u >= nch) break;  // wave-uniform
         const bool act = en[u] != kRemNone;
         const int row = (int)(en[u] >> kRemColBits);
+        // scan key: the row, and for LPE > 1 the piece (runs never cross pieces)
+        const int key = LPE == 1 ? row : ((row << 3) | q);
         f32x4 v = zv[u];
         if (!VF || a.drop_on) {
           const float w =
@@ -248,17 +306,22 @@ __global__ __launch_bounds__(kRemThreads) void k_rem_persist(StepArgs a, RemLayo
           v = f32x4{w * v.x, w * v.y, w * v.z, w * v.w};
         }
         // the previous lane's row (lane 0: none), by DPP rather than an LDS permute
-        const int prev = __builtin_amdgcn_update_dpp(-1, row, kDppWaveShr1, 0xf, 0xf, false);
-        const unsigned long long heads = __ballot(lane == 0 || prev != row || !act);
-        seg_scan(row, v, heads);
-        const bool tail = lane == kWave - 1 || ((heads >> (lane + 1)) & 1ull);
+        const int prev = __builtin_amdgcn_update_dpp(-1, key, kDppWaveShr1, 0xf, 0xf, false);
+        const unsigned long long heads = __ballot(lane == 0 || prev != key || !act);
+        seg_scan<CH>(key, v, heads);
+        const bool tail = le == CH - 1 || ((heads >> (lane + 1)) & 1ull);
         if (act && tail) {
-          const f32x4 c = acc[row];
-          acc[row] = f32x4{c.x + v.x, c.y + v.y, c.z + v.z, c.w + v.w};
+          const f32x4 c = acc[row * LPE + q];
+          acc[row * LPE + q] = f32x4{c.x + v.x, c.y + v.y, c.z + v.z, c.w + v.w};
         }
       }
     }
-    for (int r = lane; r < rows; r += kWave) rem_finish<EPI, VF>(a, L, r0 + r, acc[r]);
+    if constexpr (LPE == 1) {
+      for (int r = lane; r < rows; r += kWave) rem_finish<EPI, VF>(a, L, r0 + r, acc[r]);
+    } else {
+      for (int r = lane; r < rows * LPE; r += kWave)
+        rem_finish_piece<EPI, VF, LPE>(a, L, r0 + r / LPE, r % LPE, acc[r]);
+    }
   }
 }
 
@@ -272,7 +335,7 @@ template <bool FILL>
 __global__ __launch_bounds__(kBlock) void k_rb_walk(const int32_t* __restrict__ rp,
                                                     const int32_t* __restrict__ col,
                                                     const float* __restrict__ val, int64_t n,
-                                                    int rg, int nb, int br_log2,
+                                                    int rg, int nb, int br_log2, int chunk,
                                                     int64_t n_groups, int32_t* __restrict__ cnt,
                                                     const int32_t* __restrict__ off,
                                                     uint32_t* __restrict__ ent,
@@ -317,7 +380,7 @@ __global__ __launch_bounds__(kBlock) void k_rb_walk(const int32_t* __restrict__ 
   }
   if constexpr (!FILL) {
     for (int b = lane; b < nb; b += kWave)
-      cnt[g * nb + b] = (cur[b] + kRemChunk - 1) / kRemChunk * kRemChunk;
+      cnt[g * nb + b] = (cur[b] + chunk - 1) / chunk * chunk;
 #pragma unroll
     for (int o = 1; o < kWave; o <<= 1) nr += __shfl_xor(nr, o);
     if (lane == 0 && nr) atomicAdd(near, nr);
@@ -326,22 +389,23 @@ __global__ __launch_bounds__(kBlock) void k_rb_walk(const int32_t* __restrict__ 
 
 // cblk[c] = b for every chunk c of segment (group, block b).  Thread per segment.
 __global__ __launch_bounds__(kBlock) void k_rb_chunks(const int32_t* __restrict__ off,
-                                                      int64_t cells, int nb,
+                                                      int64_t cells, int nb, int chunk,
                                                       int32_t* __restrict__ cblk) {
   const int64_t sg = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (sg >= cells) return;
   const int b = (int)(sg % nb);
-  for (int32_t c = off[sg] / kRemChunk; c < off[sg + 1] / kRemChunk; ++c) cblk[c] = b;
+  for (int32_t c = off[sg] / chunk; c < off[sg + 1] / chunk; ++c) cblk[c] = b;
 }
 
 // H [n, ld_h] -> the split layout: main [n, fs] (whole lines per row) and rem [n, 4]
 // (columns fs..f-1, zero padded; times rem_scale[row] when given).  Thread per 16-B piece of a row (fs / 4 + 1 pieces).
 __global__ __launch_bounds__(kBlock) void k_split_copy(const float* __restrict__ h, int64_t ld_h,
-                                                       int64_t n, int f, int fs,
+                                                       int64_t n, int f, int fs, int rw,
                                                        float* __restrict__ main,
                                                        float* __restrict__ rem,
                                                        const float* __restrict__ rem_scale) {
-  const int pieces = fs / 4 + 1;
+  const int rp = rw / 4;  // 16-B pieces per remainder row
+  const int pieces = fs / 4 + rp;
   const int64_t total = n * pieces;
   for (int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * kBlock) {
@@ -351,11 +415,14 @@ __global__ __launch_bounds__(kBlock) void k_split_copy(const float* __restrict__
     if (q < fs / 4) {
       *reinterpret_cast<f32x4*>(main + row * fs + 4 * q) = ld_nt<f32x4>(p);
     } else {
-      // the remainder piece: a full 16-B read stays inside the row's storage except possibly
-      // on the buffer's last row, which reads exactly its nv valid columns
-      const int nv = f - fs;
+      // a remainder piece: a full 16-B read stays inside the row's storage except possibly
+      // on the buffer's last row, which reads exactly its nv valid columns; a piece wholly
+      // past column f (rw > 4 only) reads nothing
+      const int j = q - fs / 4;
+      const int nv = f - fs - 4 * j;
       f32x4 v = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-      if (nv == 4 || row + 1 < n) {
+      if (nv <= 0) {
+      } else if (nv >= 4 || row + 1 < n) {
         v = ld_nt<f32x4>(p);
         if (nv < 4) v.w = 0.0f;
         if (nv < 3) v.z = 0.0f;
@@ -369,20 +436,31 @@ __global__ __launch_bounds__(kBlock) void k_split_copy(const float* __restrict__
         const float d = rem_scale[row];
         v = f32x4{d * v.x, d * v.y, d * v.z, d * v.w};
       }
-      *reinterpret_cast<f32x4*>(rem + row * 4) = v;
+      *reinterpret_cast<f32x4*>(rem + row * rw + 4 * j) = v;
     }
   }
 }
 
-template <int EPI, bool VF>
+template <int EPI, bool VF, int LPE>
 hipError_t launch_rem(dim3 grid, dim3 block, size_t lds, hipStream_t s, const StepArgs& a,
                       const RemLayout& L) {
   static const hipError_t attr = hipFuncSetAttribute(  // > 64 KiB of dynamic LDS, once
-      reinterpret_cast<const void*>(k_rem_persist<EPI, kRemU, VF>),
+      reinterpret_cast<const void*>(k_rem_persist<EPI, kRemU, VF, LPE>),
       hipFuncAttributeMaxDynamicSharedMemorySize, kRemLdsBytes);
   if (attr != hipSuccess) return attr;
-  hipLaunchKernelGGL((k_rem_persist<EPI, kRemU, VF>), grid, block, lds, s, a, L);
+  hipLaunchKernelGGL((k_rem_persist<EPI, kRemU, VF, LPE>), grid, block, lds, s, a, L);
   return hipGetLastError();
+}
+
+template <int EPI, bool VF>
+hipError_t launch_rem_lpe(int lpe, dim3 grid, dim3 block, size_t lds, hipStream_t s,
+                          const StepArgs& a, const RemLayout& L) {
+  switch (lpe) {
+    case 1: return launch_rem<EPI, VF, 1>(grid, block, lds, s, a, L);
+    case 2: return launch_rem<EPI, VF, 2>(grid, block, lds, s, a, L);
+    case 4: return launch_rem<EPI, VF, 4>(grid, block, lds, s, a, L);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 // fp32 copy of dinv (the unit graph's row / column scales)
@@ -402,9 +480,12 @@ int env_or(const char* name, int dflt) {
 // The regrouped copy of A_hat for the persistent remainder pass.  Best-effort at the caller
 // (appnp_graph_create_rows): APPNP_ENOTSUP / APPNP_ERANGE / APPNP_ENOMEM leave the graph
 // without it, and appnp_propagate gathers whole rows.
-int graph_build_source_blocks(appnp_graph* g, hipStream_t s) {
+int graph_build_source_blocks(appnp_graph* g, int lpe, hipStream_t s) {
   const int64_t rows = g->row_hi - g->row_lo;
   if (g->row_lo != 0 || rows != g->n) return APPNP_EINVAL;
+  if (lpe != 1 && lpe != 2 && lpe != 4) return APPNP_EINVAL;
+  const int chunk = kRemChunk / lpe;     // entries per chunk (one per lpe lanes)
+  const int max_rg = kRemMaxRg / lpe;    // rows per wave group: 16 x max_rg x 16 lpe B of LDS
   // APPNP_SB_ROWS: measurement override of the block size (a power of two, 2^10..2^20 rows)
   static const int br_log2 = [] {
     const int x = env_or("APPNP_SB_ROWS", 1 << kSourceBlockLog2);
@@ -424,7 +505,7 @@ int graph_build_source_blocks(appnp_graph* g, hipStream_t s) {
       cus <= 0)
     return APPNP_EDEVICE;
   const int64_t slots = (int64_t)cus * kRemWaves;
-  const int64_t passes = std::max<int64_t>(1, (rows + slots * kRemMaxRg - 1) / (slots * kRemMaxRg));
+  const int64_t passes = std::max<int64_t>(1, (rows + slots * max_rg - 1) / (slots * max_rg));
   const int64_t rg = std::max<int64_t>(1, (rows + passes * slots - 1) / (passes * slots));
   const int64_t cells = passes * nb * slots;
   if (cells + 1 > INT32_MAX) return APPNP_ERANGE;
@@ -450,7 +531,8 @@ int graph_build_source_blocks(appnp_graph* g, hipStream_t s) {
       ok(hipMalloc(&tot, 2 * sizeof(int64_t))) &&
       ok(hipMemsetAsync(tot, 0, 2 * sizeof(int64_t), s))) {
     hipLaunchKernelGGL(k_rb_walk<false>, dim3(grid), dim3(kBlock), lds, s, g->row_ptr, g->col,
-                       g->val, rows, (int)rg, (int)nb, br_log2, n_groups, cnt, nullptr, nullptr,
+                       g->val, rows, (int)rg, (int)nb, br_log2, chunk, n_groups, cnt, nullptr,
+                       nullptr,
                        nullptr, reinterpret_cast<unsigned long long*>(tot + 1));
     if (ok(hipGetLastError()) && ok(exclusive_scan(cnt, cells, g->rb_off, bsum, tot, s)) &&
         ok(hipMemcpyAsync(h_tot, tot, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, s)) &&
@@ -465,9 +547,10 @@ int graph_build_source_blocks(appnp_graph* g, hipStream_t s) {
         (vf || ok(hipMemsetAsync(g->rb_val, 0, total * sizeof(float), s))) &&
         (!vf || ok(hipMalloc(&g->rb_dl, rows * sizeof(float)))) &&
         (!vf || g->mode != APPNP_NORM_SYM || ok(hipMalloc(&g->rb_dr, rows * sizeof(float)))) &&
-        ok(hipMalloc(&g->rb_cblk, std::max<int64_t>(1, total / kRemChunk) * sizeof(int32_t)))) {
+        ok(hipMalloc(&g->rb_cblk, std::max<int64_t>(1, total / chunk) * sizeof(int32_t)))) {
       hipLaunchKernelGGL(k_rb_walk<true>, dim3(grid), dim3(kBlock), lds, s, g->row_ptr, g->col,
-                         g->val, rows, (int)rg, (int)nb, br_log2, n_groups, nullptr, g->rb_off,
+                         g->val, rows, (int)rg, (int)nb, br_log2, chunk, n_groups, nullptr,
+                         g->rb_off,
                          g->rb_ent, g->rb_val, nullptr);
       if (vf && ok(hipGetLastError())) {
         const unsigned gb = (unsigned)((rows + kBlock - 1) / kBlock);
@@ -477,7 +560,7 @@ int graph_build_source_blocks(appnp_graph* g, hipStream_t s) {
       }
       if (ok(hipGetLastError()))
         hipLaunchKernelGGL(k_rb_chunks, dim3((unsigned)((cells + kBlock - 1) / kBlock)),
-                           dim3(kBlock), 0, s, g->rb_off, cells, (int)nb, g->rb_cblk);
+                           dim3(kBlock), 0, s, g->rb_off, cells, (int)nb, chunk, g->rb_cblk);
       if (ok(hipGetLastError()) && ok(hipStreamSynchronize(s)))
         g->near_frac = g->nnz_hat > 0 ? (double)h_tot[1] / (double)g->nnz_hat : 0.0;
     }
@@ -506,6 +589,7 @@ int graph_build_source_blocks(appnp_graph* g, hipStream_t s) {
   g->rb_slots = (int32_t)slots;
   g->rb_rg = (int32_t)rg;
   g->rb_passes = (int32_t)passes;
+  g->rb_lpe = lpe;
   return APPNP_OK;
 }
 
@@ -535,22 +619,24 @@ hipError_t launch_remainder(const appnp_graph* g, const StepArgs& a_in, int epi,
   const bool vf = g->rb_val == nullptr;
   RemLayout L{g->rb_off, g->rb_ent, g->rb_val, g->rb_cblk, g->rb_dl, g->rb_dr, g->rb_nb,
               g->rb_br_log2, g->rb_slots, g->rb_rg, g->rb_passes, to_rem ? 1 : 0};
-  const size_t lds = (size_t)kRemWaves * g->rb_rg * sizeof(f32x4);
+  const int lpe = g->rb_lpe;
+  const size_t lds = (size_t)kRemWaves * g->rb_rg * lpe * sizeof(f32x4);
   const dim3 grid((unsigned)g->rb_grid), block(kRemThreads);
   if (epi == EPI_BWD)
-    return vf ? launch_rem<EPI_BWD, true>(grid, block, lds, s, a, L)
-              : launch_rem<EPI_BWD, false>(grid, block, lds, s, a, L);
-  return vf ? launch_rem<EPI_FWD, true>(grid, block, lds, s, a, L)
-            : launch_rem<EPI_FWD, false>(grid, block, lds, s, a, L);
+    return vf ? launch_rem_lpe<EPI_BWD, true>(lpe, grid, block, lds, s, a, L)
+              : launch_rem_lpe<EPI_BWD, false>(lpe, grid, block, lds, s, a, L);
+  return vf ? launch_rem_lpe<EPI_FWD, true>(lpe, grid, block, lds, s, a, L)
+            : launch_rem_lpe<EPI_FWD, false>(lpe, grid, block, lds, s, a, L);
 }
 
 hipError_t launch_split_copy(const float* h, int64_t ld_h, int64_t n, int64_t f, int64_t fs,
-                             float* main, float* rem, const float* rem_scale, hipStream_t s) {
-  const int64_t total = n * (fs / 4 + 1);
+                             int64_t rw, float* main, float* rem, const float* rem_scale,
+                             hipStream_t s) {
+  const int64_t total = n * (fs / 4 + rw / 4);
   if (total <= 0) return hipSuccess;
   const int64_t blocks = std::min<int64_t>((total + kBlock - 1) / kBlock, 1 << 20);
   hipLaunchKernelGGL(k_split_copy, dim3((unsigned)blocks), dim3(kBlock), 0, s, h, ld_h, n,
-                     (int)f, (int)fs, main, rem, rem_scale);
+                     (int)f, (int)fs, (int)rw, main, rem, rem_scale);
   return hipGetLastError();
 }
 

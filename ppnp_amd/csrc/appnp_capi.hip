@@ -85,16 +85,28 @@ int env_flag(const char* name, int dflt) {
 // L2-resident passes over the source-blocked A_hat.  Returns the split point 32q, or 0 when the path does
 // not apply (no blocked copy, bf16, latency-regime graph, F outside (32, 256], vectors
 // narrower than 16 B).  APPNP_SPLIT=0 disables it (measurement).
-int64_t split_point(const appnp_graph* g, int64_t f, int dtype, int V) {
+// Remainder columns r of the split for this shape (0: rows gathered whole); the main part is
+// f - r columns (a multiple of 32, possibly 0).  r <= 4 rb_lpe: 1-4 columns on a graph built
+// with APPNP_GRAPH_SOURCE_BLOCKS, up to 8 / 16 with APPNP_GRAPH_SB_W8 / _W16, and narrow rows
+// (f <= 4 rb_lpe) run wholly in the remainder pass.
+int64_t remainder_cols(const appnp_graph* g, int64_t f, int dtype, int V) {
   static const int enabled = env_flag("APPNP_SPLIT", 1);
   if (!enabled || !g->rb_off || dtype != APPNP_F32 || V != 4) return 0;
-  if (g->n <= (1 << 16) || f <= 32 || f > 256) return 0;
+  if (g->n <= (1 << 16) || f < 1 || f > 256) return 0;
   // graphs with gather locality keep whole rows: their last line is mostly an L2 hit, cheaper
   // than the remainder pass (products-local, ~90 % near entries: 4.0 ms whole rows, 3.7 ms for
   // the 3-line main part alone, 8.5 ms split).  Uniform products-synth: 1.3 % near.
   if (g->near_frac > kSplitMaxNear && enabled != 2) return 0;  // APPNP_SPLIT=2: regardless
-  const int64_t r = f % 32;
-  return (r >= 1 && r <= 4) ? f - r : 0;
+  const int64_t w = 4 * (int64_t)g->rb_lpe;
+  const int64_t r = f > 32 ? f % 32 : f;
+  if (f <= 32 && f > w) return 0;  // one line per row already and too wide for the pass
+  return (r >= 1 && r <= w) ? r : 0;
+}
+
+// the main part of the split (columns [0, fs)), 0 when there is no split or no main part
+int64_t split_point(const appnp_graph* g, int64_t f, int dtype, int V) {
+  const int64_t r = remainder_cols(g, f, dtype, V);
+  return r ? f - r : 0;
 }
 
 // The forward loop in the split layout (appnp_blocks.hip).  Propagation is column-separable,
@@ -112,12 +124,13 @@ int propagate_split(const appnp_graph* g, const StepArgs& a0, const void* H, int
                     void* Z, int64_t ld_z, int64_t fs, int K, float p_drop, uint64_t seed,
                     char* ws, int64_t main_b, int64_t buf_b, hipStream_t s) {
   const int64_t n = a0.n_rows, f = a0.f;
+  const int lpe = g->rb_lpe, rw = 4 * lpe;  // floats per remainder row
   char* bufs[2] = {ws, ws + buf_b};
   auto main_of = [&](int i) { return reinterpret_cast<float*>(bufs[i]); };
   auto rem_of = [&](int i) { return reinterpret_cast<float*>(bufs[i] + main_b); };
   const float* h = static_cast<const float*>(H);
   float* z = static_cast<float*>(Z);
-  int rc = dev_err(appnp::launch_split_copy(h, ld_h, n, f, fs, main_of(0), rem_of(0),
+  int rc = dev_err(appnp::launch_split_copy(h, ld_h, n, f, fs, rw, main_of(0), rem_of(0),
                                             appnp::remainder_scale(g), s));
   StepArgs am = a0, ar = a0;  // main / remainder chain
   am.f = (int32_t)fs;
@@ -132,12 +145,15 @@ int propagate_split(const appnp_graph* g, const StepArgs& a0, const void* H, int
     am.zin = main_of(cur);
     am.out = last ? Z : main_of(dst);
     am.ld_out = last ? ld_z : fs;
-    rc = dev_err(appnp::launch_step(APPNP_F32, appnp::EPI_FWD, 4, am, s));
+    if (fs > 0) rc = dev_err(appnp::launch_step(APPNP_F32, appnp::EPI_FWD, 4, am, s));
     if (rc) break;
     set_drop(ar, p_drop, seed, k);
+    // LPE = 1: nv = 4 into the next remainder buffer (the shipped form); LPE > 1: nv is always
+    // the valid remainder columns, to_rem says where the row goes
+    const int nv = (lpe == 1 && !last) ? 4 : (int)(f - fs);
     rc = dev_err(appnp::launch_remainder(g, ar, appnp::EPI_FWD, rem_of(cur), h + fs, ld_h,
-                                         last ? z + fs : rem_of(dst), last ? ld_z : 4,
-                                         last ? (int)(f - fs) : 4, !last, s));
+                                         last ? z + fs : rem_of(dst), last ? ld_z : rw, nv,
+                                         !last, s));
     cur = dst;
   }
   return rc;
@@ -151,10 +167,11 @@ int propagate_bwd_split(const appnp_graph* g, const StepArgs& a0, const void* dZ
                         uint64_t seed, char* ws, int64_t main_b, int64_t buf_b,
                         hipStream_t s) {
   const int64_t n = a0.n_rows, f = a0.f;
+  const int lpe = g->rb_lpe, rw = 4 * lpe;
   char* bufs[2] = {ws, ws + buf_b};
   auto main_of = [&](int i) { return reinterpret_cast<float*>(bufs[i]); };
   auto rem_of = [&](int i) { return reinterpret_cast<float*>(bufs[i] + main_b); };
-  int rc = dev_err(appnp::launch_split_copy(static_cast<const float*>(dZ), ld_dz, n, f, fs,
+  int rc = dev_err(appnp::launch_split_copy(static_cast<const float*>(dZ), ld_dz, n, f, fs, rw,
                                             main_of(0), rem_of(0), appnp::remainder_scale(g),
                                             s));
   StepArgs am = a0, ar = a0;  // main / remainder chain
@@ -172,13 +189,13 @@ int propagate_bwd_split(const appnp_graph* g, const StepArgs& a0, const void* dZ
     am.alpha = a_k;
     am.zin = main_of(cur);
     am.out = k == 0 ? nullptr : main_of(dst);
-    rc = dev_err(appnp::launch_step(APPNP_F32, appnp::EPI_BWD, 4, am, s));
+    if (fs > 0) rc = dev_err(appnp::launch_step(APPNP_F32, appnp::EPI_BWD, 4, am, s));
     if (rc) break;
     set_drop(ar, p_drop, seed, k);
     ar.alpha = a_k;
     rc = dev_err(appnp::launch_remainder(g, ar, appnp::EPI_BWD, rem_of(cur), dh_rem, ld_dh,
-                                         k == 0 ? nullptr : rem_of(dst), 4, (int)(f - fs), true,
-                                         s));
+                                         k == 0 ? nullptr : rem_of(dst), rw, (int)(f - fs),
+                                         true, s));
     cur = dst;
   }
   return rc;
@@ -209,8 +226,12 @@ int appnp_graph_create_rows(const int32_t* indptr, const int32_t* indices, const
   *out = nullptr;
   if (n < 0 || nnz < 0 || n > INT32_MAX || nnz > INT32_MAX) return n > INT32_MAX || nnz > INT32_MAX ? APPNP_ERANGE : APPNP_EINVAL;
   const bool want_t = (mode & APPNP_GRAPH_TRANSPOSE) != 0;
-  const bool want_sb = (mode & APPNP_GRAPH_SOURCE_BLOCKS) != 0;
-  mode &= ~(APPNP_GRAPH_TRANSPOSE | APPNP_GRAPH_SOURCE_BLOCKS);
+  // remainder width of the source-blocked copy: 4 columns, or 8 / 16 (APPNP_GRAPH_SB_W8 / _W16)
+  const int sb_lpe = (mode & APPNP_GRAPH_SB_W16) ? 4 : (mode & APPNP_GRAPH_SB_W8) ? 2 : 1;
+  const bool want_sb = (mode & (APPNP_GRAPH_SOURCE_BLOCKS | APPNP_GRAPH_SB_W8 |
+                                APPNP_GRAPH_SB_W16)) != 0;
+  mode &= ~(APPNP_GRAPH_TRANSPOSE | APPNP_GRAPH_SOURCE_BLOCKS | APPNP_GRAPH_SB_W8 |
+            APPNP_GRAPH_SB_W16);
   if (mode != APPNP_NORM_SYM && mode != APPNP_NORM_RW) return APPNP_EINVAL;
   if (row_lo < 0 || row_hi < row_lo || row_hi > n) return APPNP_EINVAL;
   if (want_t && (row_lo != 0 || row_hi != n)) return APPNP_EINVAL;
@@ -227,7 +248,7 @@ int appnp_graph_create_rows(const int32_t* indptr, const int32_t* indices, const
   // Best-effort: a graph too large for the copy (block or segment count, device memory) keeps
   // whole-row gathers -- appnp_graph_source_blocks reports whether it was built.
   if (rc == APPNP_OK && want_sb && row_lo == 0 && row_hi == n) {
-    const int sb = appnp::graph_build_source_blocks(g, as_stream(stream));
+    const int sb = appnp::graph_build_source_blocks(g, sb_lpe, as_stream(stream));
     if (sb != APPNP_OK && sb != APPNP_ENOTSUP && sb != APPNP_ERANGE && sb != APPNP_ENOMEM)
       rc = sb;
   }
@@ -308,7 +329,7 @@ int appnp_graph_source_blocks(const appnp_graph* g, int64_t* bytes) {
   if (!g || !bytes) return APPNP_EINVAL;
   *bytes = 0;
   if (g->rb_off)
-    *bytes = g->rb_total * (g->rb_val ? 8 : 4) + g->rb_total / 16 +
+    *bytes = g->rb_total * (g->rb_val ? 8 : 4) + g->rb_total / 16 * g->rb_lpe +
              ((int64_t)g->rb_passes * g->rb_nb * g->rb_slots + 1) * (int64_t)sizeof(int32_t) +
              (g->rb_dl ? g->n * 4 : 0) + (g->rb_dr ? g->n * 4 : 0);
   return APPNP_OK;
@@ -317,6 +338,12 @@ int appnp_graph_source_blocks(const appnp_graph* g, int64_t* bytes) {
 int appnp_propagate_split_point(const appnp_graph* g, int64_t f, int dtype, int64_t* fs) {
   if (!g || !fs || f < 0 || !valid_dtype(dtype)) return APPNP_EINVAL;
   *fs = split_point(g, f, dtype, dtype == APPNP_F32 ? 4 : 8);
+  return APPNP_OK;
+}
+
+int appnp_propagate_remainder_cols(const appnp_graph* g, int64_t f, int dtype, int64_t* r) {
+  if (!g || !r || f < 0 || !valid_dtype(dtype)) return APPNP_EINVAL;
+  *r = remainder_cols(g, f, dtype, dtype == APPNP_F32 ? 4 : 8);
   return APPNP_OK;
 }
 
@@ -350,11 +377,13 @@ int appnp_propagate(const appnp_graph* g, const void* H, int64_t ld_h, void* Z, 
   StepArgs a = base_args(g, f, alpha);
   a.h = H;
   a.ld_h = ld_h;
-  const int64_t fs = K >= 2 ? split_point(g, f, dtype, V) : 0;
-  if (fs > 0) {
-    // two split buffers [n, fs] + [n, 4] fp32 in the workspace, each 256-B aligned
+  const int64_t r = K >= 2 ? remainder_cols(g, f, dtype, V) : 0;
+  if (r > 0) {
+    // two split buffers [n, fs] + [n, 4 rb_lpe] fp32 in the workspace, each 256-B aligned
+    // (fs = 0: narrow rows, all in the remainder pass)
+    const int64_t fs = f - r;
     const int64_t main_b = (n * fs * 4 + 255) / 256 * 256;
-    const int64_t buf_b = (main_b + n * 16 + 255) / 256 * 256;
+    const int64_t buf_b = (main_b + n * 16 * g->rb_lpe + 255) / 256 * 256;
     const size_t used = (size_t)(reinterpret_cast<uintptr_t>(ws) -
                                  reinterpret_cast<uintptr_t>(ws_orig));
     if (ws_bytes >= used + 2 * (size_t)buf_b)
@@ -421,14 +450,16 @@ int appnp_propagate_bwd(const appnp_graph* g, const void* dZ, int64_t ld_dz, voi
   rc = dev_err(appnp::launch_scale_rows(dtype, dZ, ld_dz, dH, ld_dh, n, f, alpha, s));
   if (rc) return rc;
   // split rows (self-adjoint A_hat: the source-blocked copy of A_hat is that of A_hat^T)
-  const int64_t fs = (self_adjoint && K >= 2) ? split_point(g, f, dtype, V) : 0;
+  const int64_t r = (self_adjoint && K >= 2) ? remainder_cols(g, f, dtype, V) : 0;
+  const int64_t fs = f - r;
   int64_t main_b = 0, buf_b = 0;
-  if (fs > 0) {
+  bool split = r > 0;
+  if (split) {
     main_b = (n * fs * 4 + 255) / 256 * 256;
-    buf_b = (main_b + n * 16 + 255) / 256 * 256;
+    buf_b = (main_b + n * 16 * g->rb_lpe + 255) / 256 * 256;
     const size_t used = (size_t)(reinterpret_cast<uintptr_t>(ws) -
                                  reinterpret_cast<uintptr_t>(ws_orig));
-    if (ws_bytes < used + 2 * (size_t)buf_b) main_b = 0;  // too small: whole rows
+    if (ws_bytes < used + 2 * (size_t)buf_b) split = false;  // too small: whole rows
   }
   StepArgs a = base_args(g, f, alpha);
   if (!self_adjoint) {
@@ -441,7 +472,7 @@ int appnp_propagate_bwd(const appnp_graph* g, const void* dZ, int64_t ld_dz, voi
     a.n_hub = g->t_n_hub;
   }
   a.tkey = 1;  // entry (j, i) of A_hat^T carries the mask of forward edge (i, j)
-  if (fs > 0 && main_b > 0)
+  if (split)
     return propagate_bwd_split(g, a, dZ, ld_dz, dH, ld_dh, fs, K, alpha, p_drop, seed,
                                static_cast<char*>(ws), main_b, buf_b, s);
   a.aux = dH;

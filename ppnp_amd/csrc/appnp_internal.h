@@ -56,6 +56,7 @@ struct appnp_graph {
   int32_t rb_slots = 0;         // groups per pass = rb_grid * kRemWaves
   int32_t rb_rg = 0;            // rows per group
   int32_t rb_passes = 0;
+  int32_t rb_lpe = 0;           // lanes per entry of the pass: remainder rows of 4 rb_lpe columns
   double near_frac = 0.0;       // off-diagonal entries within kNearRows of their row / nnz
 };
 
@@ -81,14 +82,17 @@ hipError_t exclusive_scan(const int32_t* cnt, int64_t rows, int32_t* out, int64_
                           int64_t* d_total, hipStream_t s);
 
 // appnp_blocks.hip
-int graph_build_source_blocks(appnp_graph* g, hipStream_t s);
+// lpe: lanes per entry of the remainder pass (1, 2, 4: remainder rows of 4, 8, 16 columns)
+int graph_build_source_blocks(appnp_graph* g, int lpe, hipStream_t s);
 // to_rem: out is the next remainder buffer (a unit graph stores dr o y there), not Z / dH
 hipError_t launch_remainder(const appnp_graph* g, const StepArgs& a, int epi,
                             const float* z_rem, const float* h_rem, int64_t ld_h, float* out,
                             int64_t ld_out, int nv, bool to_rem, hipStream_t s);
 // rem_scale (nullable): per-row factor of the remainder part (remainder_scale(g))
+// rw: floats per remainder row (4 rb_lpe)
 hipError_t launch_split_copy(const float* h, int64_t ld_h, int64_t n, int64_t f, int64_t fs,
-                             float* main, float* rem, const float* rem_scale, hipStream_t s);
+                             int64_t rw, float* main, float* rem, const float* rem_scale,
+                             hipStream_t s);
 // the factor the remainder buffers carry: dr for a value-free (unit) layout, else none
 inline const float* remainder_scale(const appnp_graph* g) {
   return g->rb_val ? nullptr : g->rb_dr;

@@ -376,13 +376,13 @@ class PartitionedAPPNP:
             from .graph import Graph
 
             # source blocks only where the rank's loop is one appnp_propagate call (column
-            # layout) on a slab whose rows split (fp32, width 32q + r, r <= 4); appnp_step
-            # gathers whole rows
-            split = (layout.rows == 1 and H.dtype == torch.float32 and n > (1 << 16)
-                     and 32 < width <= 256 and width % 32 in (1, 2, 3, 4))
+            # layout) on a slab whose rows split (graph.remainder_width: fp32, width 32q + r
+            # with r <= 16, or a narrow slab of <= 16 columns, e.g. 12-13 of F = 100 on 8
+            # ranks); appnp_step gathers whole rows
             graph = Graph.from_csr(indptr, indices, data, n, mode=mode, device=device,
                                    row_lo=lo, row_hi=hi, split_local=overlap,
-                                   source_blocks=split)
+                                   features=width if layout.rows == 1 else None,
+                                   dtype=H.dtype)
         else:
             graph = graph_fn(lo, hi, overlap)
         rows_pad = shard * layout.rows
@@ -648,11 +648,14 @@ def rank_bytes(layout: Layout, n: int, f: int, nnz_hat: int, elem_bytes: int = 4
     csr = 4 * (shard + 1) + 8 * nnz_r
     if overlap:
         csr += 4 * 2 * (shard + 1) + 8 * nnz_r
-    if R == 1 and elem_bytes == 4 and n > (1 << 16) and 32 < width <= 256 and width % 32 in (
-            1, 2, 3, 4):
-        # a column slab that takes the split-row path keeps the source-blocked copy of A_hat
-        # (8 B per nonzero plus one int per 2^15-row block and 640-row group: appnp_blocks.hip)
-        csr += 9 * nnz_hat + 4 * (-(-n // (1 << 15))) * (-(-n // 640) + 1)
+    from .graph import remainder_width
+
+    w = remainder_width(n, width, torch.float32) if R == 1 and elem_bytes == 4 else 0
+    if w:
+        # a column slab that takes the split path keeps the source-blocked copy of A_hat
+        # (8 B per nonzero plus one int per 2^15-row block and 640 / (w / 4)-row group, and
+        # padding: appnp_blocks.hip)
+        csr += 9 * nnz_hat + 4 * (-(-n // (1 << 15))) * (-(-n // (640 * 4 // w)) + 1)
     dense = (shard + 2 * shard * R) * ld * elem_bytes + (shard * ld * 4 if overlap else 0)
     return csr + 8 * n + dense
 

@@ -27,12 +27,23 @@ def _ptr(t):
     return C.c_void_p(t.data_ptr()) if t is not None and t.numel() > 0 else None
 
 
+def remainder_width(n: int, features: int, dtype=torch.float32) -> int:
+    """Columns per row (4, 8 or 16) of the source-blocked remainder pass that appnp_propagate
+    would use for this shape (appnp_capi.hip remainder_cols), 0 for whole-row gathers: fp32 rows
+    of F = 32q + r features with 1 <= r <= 16 and 32 < F <= 256, or narrow rows F <= 16, above the
+    latency regime (n > 2^16 rows).  The narrowest width that holds r."""
+    if dtype != torch.float32 or n <= (1 << 16) or not 1 <= features <= 256:
+        return 0
+    if 16 < features <= 32:
+        return 0
+    r = features % 32 if features > 32 else features
+    return next((w for w in (4, 8, 16) if 1 <= r <= w), 0)
+
+
 def splits_rows(n: int, features: int, dtype=torch.float32) -> bool:
-    """Whether appnp_propagate would take the split-row path for this shape on a graph built
-    with source blocks (appnp_capi.hip split_point): fp32 rows of F = 32q + r features with
-    1 <= r <= 4, 32 < F <= 256, above the latency regime (n > 2^16 rows)."""
-    return (dtype == torch.float32 and n > (1 << 16) and 32 < features <= 256
-            and features % 32 in (1, 2, 3, 4))
+    """Whether appnp_propagate takes the split path for this shape on a graph built with the
+    matching source-blocked copy (``remainder_width`` > 0)."""
+    return remainder_width(n, features, dtype) > 0
 
 
 class Graph:
@@ -104,11 +115,15 @@ class Graph:
             raise ValueError("indptr must have n+1 entries")
         nnz = int(ix.numel())
         row_hi = n if row_hi is None else int(row_hi)
+        width = 4
+        if features is not None and int(row_lo) == 0 and row_hi == n:
+            width = remainder_width(n, int(features), dtype) or 4
         if source_blocks is None:
             source_blocks = (features is not None and int(row_lo) == 0 and row_hi == n
                              and splits_rows(n, int(features), dtype))
+        sb_flag = {4: _lib.GRAPH_SOURCE_BLOCKS, 8: _lib.GRAPH_SB_W8, 16: _lib.GRAPH_SB_W16}[width]
         flags = ((_lib.GRAPH_TRANSPOSE if transpose else 0)
-                 | (_lib.GRAPH_SOURCE_BLOCKS if source_blocks else 0))
+                 | (sb_flag if source_blocks else 0))
         lib = _lib.load()
         out = C.c_void_p()
         with torch.cuda.device(device):
@@ -152,6 +167,15 @@ class Graph:
         _lib.check("appnp_propagate_split_point",
                    _lib.load().appnp_propagate_split_point(self._h, int(f), dt, C.byref(fs)))
         return fs.value
+
+    def remainder_cols(self, f: int, dtype=torch.float32) -> int:
+        """Columns [F - r, F) that run the L2-blocked remainder pass (r = F for narrow rows on a
+        W8 / W16 copy); 0: rows gathered whole (appnp_propagate_remainder_cols)."""
+        r = C.c_int64()
+        dt = _lib.BF16 if dtype == torch.bfloat16 else _lib.F32
+        _lib.check("appnp_propagate_remainder_cols",
+                   _lib.load().appnp_propagate_remainder_cols(self._h, int(f), dt, C.byref(r)))
+        return r.value
 
     def source_block_bytes(self) -> int:
         """Device bytes of the source-blocked copy of A_hat (0: not built)."""

@@ -1,6 +1,7 @@
 """GPU parity of the split-row path (appnp_blocks.hip): fp32 rows of F = 32q + r features,
 1 <= r <= 4, gather q cache lines and take the r remainder columns from the L2-resident pass
-over A_hat blocked by source rows (APPNP_GRAPH_SOURCE_BLOCKS).
+over A_hat blocked by source rows (APPNP_GRAPH_SOURCE_BLOCKS); with APPNP_GRAPH_SB_W8 / _W16
+the pass takes up to 8 / 16 columns, and narrow rows (F <= 8 / 16) run wholly in it.
 
 The graph has more than 2^17 nodes (three source blocks), a hub row (> 512 entries, dispatched
 first by the wide kernel) and isolated nodes.  Tolerance: the fp32 bar of test_gpu_parity.py,
@@ -263,8 +264,11 @@ def test_source_blocks_only_when_requested():
 
     a = O.synth_graph(70_000, 140_000, seed=19)
     assert ppnp_amd.Graph.from_scipy(a, device=DEV).source_block_bytes() == 0
-    assert ppnp_amd.Graph.from_scipy(a, device=DEV, features=7).source_block_bytes() == 0
+    # whole lines already (64 = 2 x 32) or one line that is too wide for the pass (17-32)
+    assert ppnp_amd.Graph.from_scipy(a, device=DEV, features=64).source_block_bytes() == 0
+    assert ppnp_amd.Graph.from_scipy(a, device=DEV, features=20).source_block_bytes() == 0
     assert ppnp_amd.Graph.from_scipy(a, device=DEV, features=100).source_block_bytes() > 0
+    assert ppnp_amd.Graph.from_scipy(a, device=DEV, features=7).source_block_bytes() > 0  # W8
 
 
 def test_source_blocks_best_effort_fallback(monkeypatch, ahat):
@@ -288,3 +292,100 @@ def test_source_blocks_best_effort_fallback(monkeypatch, ahat):
                       shape=ahat.shape)
     close_fp32(Z.double().cpu().numpy(), O.appnp_propagate(O.calc_a_hat(a, "sym"), H.numpy(), 2,
                                                            0.1))
+
+
+# ---- wider remainders: APPNP_GRAPH_SB_W8 / APPNP_GRAPH_SB_W16 (2 / 4 lanes per entry) --------
+
+
+@pytest.fixture(scope="module")
+def wide(adj):
+    """Graphs whose source-blocked copy is laid out for 8 and 16 remainder columns (chosen by
+    Graph from the named width: 40 = 32 + 8, 47 = 32 + 15)."""
+    import ppnp_amd
+
+    g8 = ppnp_amd.Graph.from_scipy(adj, device=DEV, features=40)
+    g16 = ppnp_amd.Graph.from_scipy(adj, device=DEV, features=47)
+    return {8: g8, 16: g16}
+
+
+@pytest.mark.parametrize("w,f", [(8, 40), (8, 37), (8, 8), (8, 5), (8, 3), (8, 100),
+                                 (16, 47), (16, 44), (16, 48), (16, 13), (16, 16), (16, 9),
+                                 (16, 100)])
+@pytest.mark.parametrize("K", [2, 3])
+def test_wide_remainder_matches_oracle(wide, ahat, w, f, K):
+    """Remainders of 5-16 columns and narrow rows against the float64 oracle (F = 100 on these
+    graphs: r = 4 runs the wide pass too)."""
+    import ppnp_amd
+
+    G = wide[w]
+    r = f % 32 if f > 32 else f
+    assert G.remainder_cols(f) == r and G.split_point(f) == f - r
+    H = _h(f, 40 + f + K)
+    # leading dimensions that are multiples of 4 (16-B vectors: the split path's condition)
+    ld = (f + 3) // 4 * 4
+    Hb = torch.zeros(N, ld, device=DEV)
+    Hb[:, :f] = H.to(DEV)
+    Zb = torch.empty(N, ld, device=DEV)
+    Z = ppnp_amd.propagate_forward(G, Hb[:, :f], K, 0.1, out=Zb[:, :f])
+    close_fp32(Z.double().cpu().numpy(), O.appnp_propagate(ahat, H.numpy(), K, 0.1))
+    Z2 = ppnp_amd.propagate_forward(G, Hb[:, :f], K, 0.1, out=torch.empty_like(Zb)[:, :f])
+    assert torch.equal(Z, Z2)  # deterministic
+
+
+def test_wide_remainder_limits(wide, graphs):
+    """What each layout takes: 17-32 columns and remainders wider than the layout stay whole."""
+    assert wide[8].remainder_cols(41) == 0 and wide[8].remainder_cols(12) == 0
+    assert wide[16].remainder_cols(20) == 0 and wide[16].remainder_cols(49) == 0
+    assert wide[16].remainder_cols(64) == 0 and wide[8].remainder_cols(64) == 0
+    assert graphs[0].remainder_cols(3) == 3 and graphs[0].remainder_cols(5) == 0  # W4: narrow <= 4
+    assert graphs[1].remainder_cols(3) == 0  # no copy
+
+
+@pytest.mark.parametrize("w,f,K,p", [(16, 12, 3, 0.3), (8, 40, 3, 0.25), (16, 44, 2, 0.0),
+                                     (8, 8, 4, 0.0)])
+def test_wide_remainder_dropout_and_adjoint(wide, ahat, w, f, K, p):
+    """Edge dropout (counter-hash mask) and the adjoint (transposed keys, adjoint epilogue into
+    dH's valid columns) through the wide pass, against the float64 oracle."""
+    import ppnp_amd
+
+    G = wide[w]
+    H = _h(f, 60 + f)
+    Z = ppnp_amd.propagate_forward(G, H.to(DEV), K, 0.1, p_drop=p, seed=23)
+    close_fp32(Z.double().cpu().numpy(),
+               O.appnp_propagate(ahat, H.numpy(), K, 0.1, p_drop=p, seed=23))
+    dH = ppnp_amd.propagate_backward(G, H.to(DEV), K, 0.1, p_drop=p, seed=23)
+    close_fp32(dH.double().cpu().numpy(),
+               O.appnp_backward(ahat, H.numpy(), K, 0.1, p_drop=p, seed=23))
+
+
+def test_wide_remainder_padded_views(wide, ahat):
+    """Narrow rows as column views of wider buffers (F = 13 in ld 16 / 20): the padding columns
+    of Z stay untouched and H's padding is never read into the result."""
+    import ppnp_amd
+
+    f = 13
+    H = _h(f, 71)
+    Hb = torch.full((N, 16), float("nan"), device=DEV)
+    Hb[:, :f] = H.to(DEV)
+    Zb = torch.full((N, 20), 5.0, device=DEV)
+    Z = ppnp_amd.propagate_forward(wide[16], Hb[:, :f], 3, 0.1, out=Zb[:, :f])
+    close_fp32(Z.double().cpu().numpy(), O.appnp_propagate(ahat, H.numpy(), 3, 0.1))
+    assert bool((Zb[:, f:] == 5.0).all())
+
+
+@pytest.mark.parametrize("mode", ["sym", "rw"])
+def test_wide_remainder_weighted_and_rw(adj, mode):
+    """Values in the wide copy (weighted graph) and 'rw' normalisation."""
+    import ppnp_amd
+
+    wgt = adj.copy()
+    rng = np.random.default_rng(29)
+    wgt.data = rng.uniform(0.5, 2.0, size=wgt.nnz).astype(np.float32)
+    wgt = ((wgt + wgt.T) * 0.5).tocsr()
+    wgt.sort_indices()
+    G = ppnp_amd.Graph.from_scipy(wgt, mode=mode, device=DEV, features=44)
+    assert G.remainder_cols(44) == 12
+    H = _h(44, 33)
+    Z = ppnp_amd.propagate_forward(G, H.to(DEV), 3, 0.15, p_drop=0.2, seed=7)
+    ref = O.appnp_propagate(O.calc_a_hat(wgt, mode), H.numpy(), 3, 0.15, p_drop=0.2, seed=7)
+    close_fp32(Z.double().cpu().numpy(), ref)
