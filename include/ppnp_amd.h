@@ -71,8 +71,9 @@ enum appnp_norm { APPNP_NORM_SYM = 0, APPNP_NORM_RW = 1 };
 
 /* OR into `mode` instead of (or with) APPNP_GRAPH_SOURCE_BLOCKS: the source-blocked copy for a
  * remainder of up to 8 (W8) or 16 (W16) columns: fp32 rows of F = 32q + r features with
- * r <= 8 / 16, and narrow rows F <= 8 / 16 whole (for example the 12-13-column slabs of an
- * 8-rank column layout of F = 100, or F = 40 = 32 + 8).  The pass then gives 2 / 4 lanes to each
+ * r <= 8 (a wider remainder beside a main part costs as much as its extra line, measured), and
+ * narrow rows F <= 8 / 16 whole (for example F = 40 = 32 + 8, or the 12-13-column slabs of an
+ * 8-rank column layout of F = 100).  The pass then gives 2 / 4 lanes to each
  * entry and holds 320 / 160 rows per wave group, so a graph may need 2 / 4 row passes per
  * launch.  Same memory as APPNP_GRAPH_SOURCE_BLOCKS (segments padded to 32 / 16 entries). */
 #define APPNP_GRAPH_SB_W8 0x400
@@ -183,8 +184,8 @@ size_t appnp_workspace_bytes(const appnp_graph* g, int64_t f, int64_t ld, int dt
 int appnp_propagate_split_point(const appnp_graph* g, int64_t f, int dtype, int64_t* fs);
 
 /* The remainder columns of that split: *r = F - fs columns run the L2-blocked pass (1-4, or
- * up to 8 / 16 on a graph built with APPNP_GRAPH_SB_W8 / _W16, where narrow rows F <= 8 / 16
- * run wholly in the pass, with *fs = 0); *r = 0 when rows are gathered whole. */
+ * up to 8 on a graph built with APPNP_GRAPH_SB_W8 / _W16, where narrow rows F <= 8 / 16 run
+ * wholly in the pass, with *fs = 0); *r = 0 when rows are gathered whole. */
 int appnp_propagate_remainder_cols(const appnp_graph* g, int64_t f, int dtype, int64_t* r);
 
 /*

@@ -50,9 +50,10 @@
 // W = 4 LPE fp32 columns, LPE = 2 or 4 lanes per entry, laid out piece-major (lane = piece * CH +
 // entry, CH = 64 / LPE entries per chunk), so every 16-lane DPP row holds one 16-B piece of up to
 // 16 consecutive entries and the segmented scan compares (row, piece).  A wave group holds
-// 640 / LPE rows.  It takes 5-16 remainder columns (F = 32q + r) and narrow rows (F <= W) out
-// of the random gather (tools/blk_probe.hip: 16 columns of products' shape 1.89 against 2.38 ms
-// per pass).  LPE = 1 is the pass above, unchanged.
+// 640 / LPE rows.  It takes 5-8 remainder columns (F = 32q + r) and narrow rows (F <= W) out
+// of the random gather: on products-synth F = 16 takes 2.01 against 2.40 ms per iteration and
+// F = 40 = 32 + 8 3.68 against 4.44 ms (profiles/r2_wide_remainder.txt).
+// LPE = 1 is the pass above, unchanged.
 #include <algorithm>
 #include <cstdlib>
 

@@ -100,6 +100,10 @@ int64_t remainder_cols(const appnp_graph* g, int64_t f, int dtype, int V) {
   const int64_t w = 4 * (int64_t)g->rb_lpe;
   const int64_t r = f > 32 ? f % 32 : f;
   if (f <= 32 && f > w) return 0;  // one line per row already and too wide for the pass
+  // beside a main part, a remainder of 9-16 columns costs as much as its extra line
+  // (products-synth F = 47: 4.53 ms split against 4.41 ms whole rows; F = 40 = 32 + 8: 3.68
+  // against 4.44 ms; profiles/r2_wide_remainder.txt)
+  if (f > 32 && r > 8) return 0;
   return (r >= 1 && r <= w) ? r : 0;
 }
 

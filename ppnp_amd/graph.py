@@ -30,13 +30,15 @@ def _ptr(t):
 def remainder_width(n: int, features: int, dtype=torch.float32) -> int:
     """Columns per row (4, 8 or 16) of the source-blocked remainder pass that appnp_propagate
     would use for this shape (appnp_capi.hip remainder_cols), 0 for whole-row gathers: fp32 rows
-    of F = 32q + r features with 1 <= r <= 16 and 32 < F <= 256, or narrow rows F <= 16, above the
+    of F = 32q + r features with 1 <= r <= 8 and 32 < F <= 256, or narrow rows F <= 16, above the
     latency regime (n > 2^16 rows).  The narrowest width that holds r."""
     if dtype != torch.float32 or n <= (1 << 16) or not 1 <= features <= 256:
         return 0
     if 16 < features <= 32:
         return 0
     r = features % 32 if features > 32 else features
+    if features > 32 and r > 8:
+        return 0  # beside a main part, 9-16 columns cost their extra line (appnp_capi.hip)
     return next((w for w in (4, 8, 16) if 1 <= r <= w), 0)
 
 

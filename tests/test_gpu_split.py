@@ -300,11 +300,12 @@ def test_source_blocks_best_effort_fallback(monkeypatch, ahat):
 @pytest.fixture(scope="module")
 def wide(adj):
     """Graphs whose source-blocked copy is laid out for 8 and 16 remainder columns (chosen by
-    Graph from the named width: 40 = 32 + 8, 47 = 32 + 15)."""
+    Graph from the named width: 40 = 32 + 8, narrow rows of 13)."""
     import ppnp_amd
 
     g8 = ppnp_amd.Graph.from_scipy(adj, device=DEV, features=40)
-    g16 = ppnp_amd.Graph.from_scipy(adj, device=DEV, features=47)
+    g16 = ppnp_amd.Graph.from_scipy(adj, device=DEV, features=13)
+    assert g8.source_block_bytes() > 0 and g16.source_block_bytes() > 0
     return {8: g8, 16: g16}
 
 
@@ -313,13 +314,15 @@ def wide(adj):
                                  (16, 100)])
 @pytest.mark.parametrize("K", [2, 3])
 def test_wide_remainder_matches_oracle(wide, ahat, w, f, K):
-    """Remainders of 5-16 columns and narrow rows against the float64 oracle (F = 100 on these
-    graphs: r = 4 runs the wide pass too)."""
+    """Remainders of 5-8 columns and narrow rows against the float64 oracle (F = 100 on these
+    graphs: r = 4 runs the wide pass too; 47, 44, 48 = 32 + 9..16 keep whole rows)."""
     import ppnp_amd
 
     G = wide[w]
     r = f % 32 if f > 32 else f
-    assert G.remainder_cols(f) == r and G.split_point(f) == f - r
+    if f > 32 and r > 8:
+        r = 0
+    assert G.remainder_cols(f) == r and G.split_point(f) == (f - r if r else 0)
     H = _h(f, 40 + f + K)
     # leading dimensions that are multiples of 4 (16-B vectors: the split path's condition)
     ld = (f + 3) // 4 * 4
@@ -336,12 +339,13 @@ def test_wide_remainder_limits(wide, graphs):
     """What each layout takes: 17-32 columns and remainders wider than the layout stay whole."""
     assert wide[8].remainder_cols(41) == 0 and wide[8].remainder_cols(12) == 0
     assert wide[16].remainder_cols(20) == 0 and wide[16].remainder_cols(49) == 0
+    assert wide[16].remainder_cols(47) == 0 and wide[16].remainder_cols(40) == 8
     assert wide[16].remainder_cols(64) == 0 and wide[8].remainder_cols(64) == 0
     assert graphs[0].remainder_cols(3) == 3 and graphs[0].remainder_cols(5) == 0  # W4: narrow <= 4
     assert graphs[1].remainder_cols(3) == 0  # no copy
 
 
-@pytest.mark.parametrize("w,f,K,p", [(16, 12, 3, 0.3), (8, 40, 3, 0.25), (16, 44, 2, 0.0),
+@pytest.mark.parametrize("w,f,K,p", [(16, 12, 3, 0.3), (8, 40, 3, 0.25), (16, 16, 2, 0.0),
                                      (8, 8, 4, 0.0)])
 def test_wide_remainder_dropout_and_adjoint(wide, ahat, w, f, K, p):
     """Edge dropout (counter-hash mask) and the adjoint (transposed keys, adjoint epilogue into
@@ -383,9 +387,9 @@ def test_wide_remainder_weighted_and_rw(adj, mode):
     wgt.data = rng.uniform(0.5, 2.0, size=wgt.nnz).astype(np.float32)
     wgt = ((wgt + wgt.T) * 0.5).tocsr()
     wgt.sort_indices()
-    G = ppnp_amd.Graph.from_scipy(wgt, mode=mode, device=DEV, features=44)
-    assert G.remainder_cols(44) == 12
-    H = _h(44, 33)
+    G = ppnp_amd.Graph.from_scipy(wgt, mode=mode, device=DEV, features=40)
+    assert G.remainder_cols(40) == 8
+    H = _h(40, 33)
     Z = ppnp_amd.propagate_forward(G, H.to(DEV), 3, 0.15, p_drop=0.2, seed=7)
     ref = O.appnp_propagate(O.calc_a_hat(wgt, mode), H.numpy(), 3, 0.15, p_drop=0.2, seed=7)
     close_fp32(Z.double().cpu().numpy(), ref)
