@@ -393,3 +393,23 @@ def test_wide_remainder_weighted_and_rw(adj, mode):
     Z = ppnp_amd.propagate_forward(G, H.to(DEV), 3, 0.15, p_drop=0.2, seed=7)
     ref = O.appnp_propagate(O.calc_a_hat(wgt, mode), H.numpy(), 3, 0.15, p_drop=0.2, seed=7)
     close_fp32(Z.double().cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("f", [3, 4])
+def test_narrow_rows_on_the_four_column_layout(graphs, ahat, f):
+    """F <= 4 on the shipped 4-column copy: no main part (fs = 0), every column in the pass
+    (LPE = 1), forward and adjoint against the float64 oracle."""
+    import ppnp_amd
+
+    G = graphs[0]
+    assert G.remainder_cols(f) == f and G.split_point(f) == 0
+    H = _h(f, 80 + f)
+    Hb = torch.zeros(N, 4, device=DEV)
+    Hb[:, :f] = H.to(DEV)
+    Zb = torch.full((N, 4), 9.0, device=DEV)
+    Z = ppnp_amd.propagate_forward(G, Hb[:, :f], 3, 0.1, out=Zb[:, :f])
+    close_fp32(Z.double().cpu().numpy(), O.appnp_propagate(ahat, H.numpy(), 3, 0.1))
+    assert bool((Zb[:, f:] == 9.0).all())
+    if f == 4:  # the adjoint makes dZ contiguous: ld 4 keeps the 16-B vectors
+        dH = ppnp_amd.propagate_backward(G, H.to(DEV), 3, 0.1)
+        close_fp32(dH.double().cpu().numpy(), O.appnp_backward(ahat, H.numpy(), 3, 0.1))
