@@ -4,30 +4,43 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload products-synth]
 
 A "step" is one full propagation call -- K=10 fused SpMM+AXPBY iterations over the whole
-graph (appnp_propagate, or the row-partitioned multi-GPU loop) -- on synthetic input that is
+graph (appnp_propagate, or the partitioned multi-GPU loop) -- on synthetic input that is
 resident in HBM before the timed region.  value = nodes * F * K * steps / time (whole job).
 
 N > 1 (launched by torch.distributed.run, one rank per GPU): the ranks form an R x C layout
 (ppnp_amd/dist.py): C feature slabs need no exchange, R row groups
-exchange their Z shards over RCCL every iteration.  --layout auto times the candidate layouts
-of ppnp_amd.dist.candidate_layouts after warm-up (max over ranks) and keeps the fastest; the
-timed region is bracketed by barrier + synchronize and the max over ranks is reported.
+exchange their Z shards over RCCL every iteration.  --layout auto measures every candidate
+layout of ppnp_amd.dist.candidate_layouts with the full protocol (W warm-up steps, then exactly
+K timed steps bracketed by barrier + synchronize, max over ranks, parity of the result) and
+prints the fastest one whose parity holds.  The candidate without a data-path exchange (the
+column layout) is measured first, and every later candidate runs under a deadline
+(--candidate-timeout): if an exchange stalls, the RCCL communicators are aborted, rank 0
+prints the best line measured so far, and every rank exits -- the scaling run always gets a
+line unless the exchange-free layout itself fails.
 
 Extra JSON fields:
-  roofline      HBM roofline of the dominant kernel (k_step_*): algorithmic bytes per launch
-                B_iter = 4(N+1) + 8 nnz(A_hat) + 3 N F s   / average
-                launch time, measured with HIP events on the launch stream; peak 8 TB/s.
-  cpu_baseline  the oracle's torch.sparse.mm CPU loop (oracle/ppnp_oracle.py) on the same graph
-                and H, a bounded number of iterations, rank 0 at N=1 only.
+  roofline      HBM roofline of the iteration's kernels on one rank: algorithmic bytes per
+                iteration B_iter = 4(rows+1) + 8 nnz(A_hat rows) + (n + 2 rows) F s (SURVEY.md
+                section 8(d), restricted to the rank's share) / the average iteration time,
+                measured with HIP events on the launch stream; peak 8 TB/s.  ``ceiling`` is
+                the access-pattern lower bound on the iteration time (line requests beyond L2
+                at the fastest measured random-line rate; exchange at the xGMI link peak).
+  cpu_baseline  the oracle's torch.sparse.mm CPU loop (oracle/ppnp_oracle.py) on the same
+                graph and H, rank 0, after the first timed region (N = 1 and N > 1).
+  parity        the timed Z_K against the CPU loop (N = 1) or, per rank, its block against a
+                single-GPU propagation of the whole graph (N > 1; max over ranks).
 """
 
 from __future__ import annotations
 
 import argparse
 import datetime
+import glob
+import hashlib
 import json
 import os
 import sys
+import threading
 import time
 
 import torch
@@ -37,12 +50,15 @@ sys.path.insert(0, ROOT)
 
 METRIC = "APPNP K=10 propagated node-feats/sec; achieved HBM GB/s vs peak, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip-level parameters)
-# random row-gather ceiling measured on MI355X: ~54-57 G cache-line requests/s for 64-512 B
-# rows from a 1 GB table (profiles/r1_gather_probe.txt)
-GATHER_LINE_CEILING = 56.0
+# random row-gather rate: 53-60 G cache-line requests/s for 64-512 B rows from 64 MB-1 GB
+# tables, Infinity-Cache hits or not (tools/gather_probe.hip, profiles/r1_gather_probe.txt).
+# The ceiling uses the fastest measured rate, so it is a lower bound on the iteration time.
+GATHER_LINE_CEILING = 60.0
+# xGMI: 7 links per GPU at 76.8 GB/s per direction (153.6 GB/s bidirectional)
+XGMI_IN_GBS = 7 * 76.8
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)  # median of >= 20 after 3 warm-ups
@@ -65,21 +81,13 @@ def parse():
                         "(appnp_plan_*; for small, launch-bound workloads)")
     p.add_argument("--overlap", action="store_true",
                    help="row layouts: overlap the all-gather with the local-column product")
-    p.add_argument("--exchange", default="multipath", choices=["multipath", "group"],
+    p.add_argument("--exchange", default="multipath", choices=["multipath", "group", "native"],
                    help="R x C layouts: relayed exchange over every rank, or one all-gather "
-                        "per column group")
-    return p.parse_args()
-
-
-def committed_traffic(workload, dtype, parallelism):
-    """HBM bytes per launch of the SpMM kernel from the committed PMC profile of the same
-    command (tools/summarize_profile.py writes profiles/pmc_traffic.json), or None."""
-    key = f"{workload}:{'bf16' if dtype == torch.bfloat16 else 'f32'}:{parallelism}"
-    try:
-        with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as fh:
-            return json.load(fh).get(key)
-    except (OSError, ValueError):
-        return None
+                        "per column group; row layouts: 'native' runs the library's own loop")
+    p.add_argument("--candidate-timeout", type=float, default=240.0,
+                   help="N > 1: seconds one layout candidate (build, warm-up, timed steps, "
+                        "parity) may take before the run is ended with the best line so far")
+    return p.parse_args(argv)
 
 
 def log(*a):
@@ -106,6 +114,31 @@ def cpu_threads() -> tuple[int, int]:
     return max(1, min(visible, share)), visible
 
 
+def src_digest() -> str:
+    """Digest of the HIP sources: keys the committed PMC traffic to the kernels that made it."""
+    h = hashlib.sha1()
+    for p in sorted(glob.glob(os.path.join(ROOT, "ppnp_amd", "csrc", "*.hip"))
+                    + glob.glob(os.path.join(ROOT, "ppnp_amd", "csrc", "*.h"))):
+        with open(p, "rb") as fh:
+            h.update(os.path.basename(p).encode() + fh.read())
+    return h.hexdigest()[:12]
+
+
+def traffic_key(workload, dtype_name, parallelism, kernel_key) -> str:
+    return f"{workload}:{dtype_name}:{parallelism}:{kernel_key}:src={src_digest()}"
+
+
+def committed_traffic(key):
+    """HBM bytes per iteration from the committed PMC profile of the same command, kernels and
+    kernel sources (tools/summarize_profile.py writes profiles/pmc_traffic.json), or None: a
+    profile of other kernels or of an older build of them never matches the key."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as fh:
+            return json.load(fh).get(key)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(graph, H, K, alpha, iters, adj=None):
     """Time the oracle's CPU torch.sparse.mm APPNP loop on the same operator and H (SURVEY.md
     8(d) CPU baseline (i)); return (the JSON object, Z of the CPU loop).  For N <= 20k also time
@@ -118,6 +151,7 @@ def cpu_baseline(graph, H, K, alpha, iters, adj=None):
     rp, col, val, _ = graph.csr()
     a_t = torch.sparse_csr_tensor(rp.cpu().long(), col.cpu().long(), val.cpu(),
                                   size=(graph.n, graph.n))
+    del rp, col, val
     Hc = H.float().cpu()
     t0 = time.perf_counter()
     Zc = O.appnp_propagate_torch_cpu(a_t, Hc, iters, alpha)
@@ -154,67 +188,293 @@ def cpu_baseline(graph, H, K, alpha, iters, adj=None):
     return res, Zc
 
 
-def tune_layouts(cands, indptr, indices, n, H, K, alpha, dev, ctl, reps=2):
-    """Build each candidate layout, time ``reps`` propagations after one warm-up (barrier on
-    both sides, max over ranks: every rank sees the same numbers and picks the same layout),
-    keep the fastest and free the others.  A candidate that raises on any rank (agreed over the
-    gloo control group ``ctl``, which an RCCL error cannot poison) is recorded as failed and
-    skipped, so one broken exchange does not cost the whole scaling run."""
-    from ppnp_amd import dist as pdist
+# ---------------------------------------------------------------------------------------------
+# roofline of one rank's iteration
+# ---------------------------------------------------------------------------------------------
 
-    best, best_ms, times = None, None, {}
-    for layout, overlap, exchange in cands:
-        name = (f"rows{layout.rows}xcols{layout.cols}" + ("-overlap" if overlap else "")
-                + (f"-{exchange}" if (layout.rows > 1 and layout.cols > 1)
-                   or exchange == "native" else ""))
-        if torch.distributed.get_rank() == 0:
-            log(f"[bench] autotune: building {layout} overlap={overlap} exchange={exchange}")
-        r, err, dt = None, "", 0.0
+
+def kernel_plan(F_local, K, remainder_cols, sb):
+    """What one iteration runs on this rank: (description, key, fs, r, lpe).  ``remainder_cols``
+    is the split the runner actually takes (0: whole rows through the SpMM kernel); ``sb`` the
+    graph's source-blocked layout (Graph.source_block_layout)."""
+    r = int(remainder_cols) if K >= 2 and sb else 0
+    if not r:
+        return ("k_step (one fused SpMM launch per iteration)", "k_step", F_local, 0, 1)
+    fs = F_local - r
+    lpe = sb["width"] // 4
+    rem = f"k_rem_persist<W{sb['width']}{',vf' if sb['value_free'] else ''}>"
+    if not fs:
+        return (f"{rem} on all {F_local} columns (narrow rows: one persistent L2-blocked launch "
+                f"per iteration, {sb['row_passes']} row passes)", f"{rem}[0,{F_local})", 0, r,
+                lpe)
+    return (f"k_step on columns [0, {fs}) + {rem} on the remainder columns [{fs}, {F_local}) "
+            "(one persistent L2-blocked launch) per iteration; times are per iteration",
+            f"k_step[0,{fs})+{rem}[{fs},{F_local})", fs, r, lpe)
+
+
+def roofline(*, n, rows, nnz, F_local, esz, avg_iter_ms, fs, r, lpe, rb_total=0,
+             rb_entry_bytes=4, exchange_in_bytes=0, kernel="", kernel_key="", traffic=None):
+    """The roofline block of one rank.
+
+    achieved = B_iter / iteration time with B_iter = 4(rows+1) + 8 nnz + (n + 2 rows) F s: the
+    rank's A_hat rows once, all n rows of its slab of Z_k once (a row-layout rank gathers every
+    row), H and Z_{k+1} of its rows once.  For one GPU this is SURVEY 8(d)'s 4(N+1)+8nnz+3NFs.
+
+    ceiling = the iteration's line requests beyond L2 at the fastest measured random-line rate:
+    ``lines_per_nonzero`` gathered 128-B lines per nonzero of the SpMM kernel (whole lines of the
+    fs main columns, or all of a whole row), plus every streamed byte (CSR, the remainder pass's
+    regrouped entries, H, Z) / 128; the remainder pass's gathers are L2 requests and are not
+    counted.  A row layout's exchange adds max(compute bound, exchange bytes / xGMI link peak).
+    A lower bound on the time, so ceiling.frac >= frac on a uniform random graph; a graph with
+    gather locality (L2 hits) can beat it, and then the ceiling is clamped to the measured time
+    and says so."""
+    from ppnp_amd.dist import _avg_lines, line_ld
+
+    s = esz
+    b_iter = 4 * (rows + 1) + 8 * nnz + (n + 2 * rows) * F_local * s
+    achieved = b_iter / (avg_iter_ms * 1e-3) / 1e9 if avg_iter_ms > 0 else 0.0
+    if r:
+        lpn = fs * s // 128
+        stream = (4 * (rows + 1) + 8 * nnz if fs else 0) + rb_total * rb_entry_bytes
+        ld_main = fs
+        dense = 2 * rows * fs * s + 2 * rows * 16 * lpe
+    else:
+        ld = line_ld(F_local, s)
+        lpn = _avg_lines(F_local * s, ld * s)
+        stream = 4 * (rows + 1) + 8 * nnz
+        ld_main = ld
+        dense = 2 * rows * ld_main * s
+    lines = nnz * lpn + (stream + dense) / 128
+    compute_ms = lines / (GATHER_LINE_CEILING * 1e9) * 1e3
+    exchange_ms = exchange_in_bytes / (XGMI_IN_GBS * 1e9) * 1e3
+    ceil_ms = max(compute_ms, exchange_ms)
+    note = ("a uniform random graph gathers whole cache lines per nonzero, so the "
+            "compulsory-byte fraction is capped at ceiling.frac; 60 % of the compulsory-byte "
+            "roofline is out of reach for it on one GPU")
+    clamped = avg_iter_ms > 0 and ceil_ms > avg_iter_ms
+    if clamped:
+        ceil_ms = avg_iter_ms
+        note = ("measured faster than the uniform-gather bound (gather locality: L2 hits), so "
+                "the ceiling is the measured time")
+    line_rate = lines / (avg_iter_ms * 1e-3) / 1e9 if avg_iter_ms > 0 else 0.0
+    tgbs = traffic / (avg_iter_ms * 1e-3) / 1e9 if traffic and avg_iter_ms > 0 else None
+    return {
+        "bound": "hbm",
+        "achieved": achieved,
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": achieved / HBM_PEAK_GBS,
+        "traffic": traffic,
+        "traffic_source": "profiles/pmc_traffic.json: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
+                          "passes of this command, kernels and kernel sources (key "
+                          "roofline.traffic_key), gfx950-corrected; null when none matches",
+        "traffic_GBs": tgbs,
+        "traffic_frac": tgbs / HBM_PEAK_GBS if tgbs else None,
+        "gather_line_rate": {
+            "lines_per_iter": lines,
+            "achieved_G_lines_s": line_rate,
+            "ceiling_G_lines_s": GATHER_LINE_CEILING,
+            "frac": line_rate / GATHER_LINE_CEILING,
+            "ceiling_source": "tools/gather_probe.hip, profiles/r1_gather_probe.txt",
+        },
+        "kernel": kernel,
+        "kernel_key": kernel_key,
+        "bytes_per_launch": b_iter,
+        "avg_launch_ms": avg_iter_ms,
+        "ceiling": {
+            "ms_per_iter": ceil_ms,
+            "frac": b_iter / (ceil_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if ceil_ms > 0 else None,
+            "lines_per_nonzero": lpn,
+            "remainder_l2_requests_per_nonzero": lpe if r else 0,
+            "compute_ms": compute_ms,
+            "exchange_ms": exchange_ms,
+            "exchange_in_bytes": exchange_in_bytes,
+            "clamped_to_measured": clamped,
+            "basis": f"{lines:.4g} line requests per iteration at {GATHER_LINE_CEILING} G "
+                     f"lines/s; exchange {exchange_in_bytes / 1e6:.4g} MB in at "
+                     f"{XGMI_IN_GBS:.0f} GB/s",
+        },
+        "note": note,
+    }
+
+
+# ---------------------------------------------------------------------------------------------
+# timing protocol
+# ---------------------------------------------------------------------------------------------
+
+
+def time_steps(run, stream, steps, warmup, world, ctl):
+    """W untimed warm-up steps, then exactly ``steps`` timed steps bracketed by barrier +
+    synchronize on both sides; HIP events on the launch stream give the device time and the
+    spread of the steps.  Max over ranks."""
+    for _ in range(warmup):
+        run()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier(group=ctl)
+    torch.cuda.synchronize()
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+    t0 = time.perf_counter()
+    evs[0].record(stream)
+    for i in range(steps):
+        run()
+        evs[i + 1].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier(group=ctl)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    dev_ms = evs[0].elapsed_time(evs[-1])
+    steps_ms = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(steps))
+    if world > 1:
+        t = torch.tensor([wall, dev_ms], dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX, group=ctl)
+        wall, dev_ms = float(t[0]), float(t[1])
+    return wall, dev_ms, steps_ms
+
+
+class Deadline:
+    """Wall-clock deadline of one layout candidate.  If it expires, ``on_expire`` runs on the
+    timer thread (it never returns: it ends the process).  ``finish`` disarms it; the lock makes
+    finish and expiry mutually exclusive."""
+
+    def __init__(self, seconds, on_expire):
+        self.lock = threading.Lock()
+        self.done = False
+        self.on_expire = on_expire
+        self.timer = threading.Timer(seconds, self._fire)
+        self.timer.daemon = True
+
+    def _fire(self):
+        with self.lock:
+            if self.done:
+                return
+            self.on_expire()
+
+    def __enter__(self):
+        self.timer.start()
+        return self
+
+    def __exit__(self, *exc):
+        with self.lock:
+            self.done = True
+        self.timer.cancel()
+        return False
+
+
+def _abort_rccl():
+    """Abort every process group (ncclCommAbort for RCCL ones): stalled collective kernels
+    exit, so the process can end without waves left spinning on the GPU."""
+    try:
+        torch.distributed.distributed_c10d._abort_process_group()
+    except Exception as e:  # noqa: BLE001 -- best effort on the way out
+        log(f"[bench] process-group abort: {type(e).__name__}: {e}")
+
+
+def run_candidates(cands, measure, ctl, timeout_s, emit, name_of, rank, world,
+                   abort=_abort_rccl, exit_fn=os._exit):
+    """Measure every candidate in order and return (best result, {name: ms per step or None}).
+
+    ``measure(cand)`` builds the candidate, times it (``time_steps``), checks parity and returns
+    its result dict (``ms_per_step``, ``parity.ok``).  A candidate that raises on any rank
+    (agreed over the gloo control group ``ctl``, which an RCCL error cannot poison) or fails
+    parity is recorded and skipped.  Every candidate after the first runs under a deadline of
+    ``timeout_s``: on expiry the RCCL communicators are aborted, rank 0 ``emit``s the best
+    result so far (autotune marked "timeout") and the process ends through ``exit_fn`` -- the
+    same on every rank, whose deadlines expire together.  The first candidate is the layout
+    without a data-path exchange, so it has no deadline."""
+    best, times = None, {}
+    for i, cand in enumerate(cands):
+        name = name_of(cand)
+        if rank == 0:
+            log(f"[bench] candidate {name}: building and timing")
+
+        def expire(name=name):
+            log(f"[bench] candidate {name} passed its {timeout_s:.0f} s deadline on rank "
+                f"{rank}: aborting the exchange, keeping the best line so far")
+            t = threading.Thread(target=abort, daemon=True)
+            t.start()
+            t.join(30)
+            times[name] = "timeout"
+            if rank == 0 and best is not None:
+                best["config"]["autotune_ms_per_step"] = dict(times)
+                emit(best)
+            exit_fn(0 if best is not None else 3)
+
+        res, err = None, ""
+        guard = Deadline(timeout_s, expire) if i > 0 and timeout_s > 0 else None
+        if guard:
+            guard.__enter__()
         try:
-            r = pdist.PartitionedAPPNP.create(indptr, indices, n, H, K, alpha, dev,
-                                              layout=layout, overlap=overlap, exchange=exchange)
-            r.run()
-            torch.cuda.synchronize()
-        except Exception as e:  # noqa: BLE001 -- reported and agreed on below
-            err = f"{type(e).__name__}: {e}"
-        failed = torch.tensor([1.0 if err else 0.0], dtype=torch.float64)
-        torch.distributed.all_reduce(failed, op=torch.distributed.ReduceOp.MAX, group=ctl)
-        if float(failed) == 0.0:
-            torch.distributed.barrier(group=ctl)
-            t0 = time.perf_counter()
             try:
-                for _ in range(reps):
-                    r.run()
-                torch.cuda.synchronize()
-                dt = time.perf_counter() - t0
-            except Exception as e:  # noqa: BLE001
+                res = measure(cand)
+            except Exception as e:  # noqa: BLE001 -- reported and agreed on below
                 err = f"{type(e).__name__}: {e}"
-            t = torch.tensor([dt, 1.0 if err else 0.0], dtype=torch.float64)
-            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX, group=ctl)
-            dt, failed = float(t[0]), t[1:]
+            failed = torch.tensor([1.0 if err else 0.0], dtype=torch.float64)
+            if world > 1:
+                torch.distributed.all_reduce(failed, op=torch.distributed.ReduceOp.MAX,
+                                             group=ctl)
+        finally:
+            if guard:
+                guard.__exit__(None, None, None)
         if float(failed) != 0.0:
             times[name] = None
-            log(f"[bench] autotune {name}: FAILED on rank {torch.distributed.get_rank()}"
+            log(f"[bench] candidate {name}: FAILED on rank {rank}"
                 + (f": {err}" if err else " (another rank failed)"))
-            del r
-            torch.cuda.empty_cache()
             continue
-        ms = dt * 1e3 / reps
-        times[name] = ms
-        if torch.distributed.get_rank() == 0:
-            log(f"[bench] autotune {name}: {ms:.3f} ms per propagation")
-        if best_ms is None or ms < best_ms:
-            best, best_ms = r, ms
-        else:
-            del r
-        torch.cuda.empty_cache()
+        ok = res.get("parity", {}).get("ok", True)
+        times[name] = res["ms_per_step"]
+        if rank == 0:
+            log(f"[bench] candidate {name}: {res['ms_per_step']:.3f} ms per step"
+                + ("" if ok else " -- PARITY FAILURE, not eligible"))
+        if ok and (best is None or res["ms_per_step"] < best["ms_per_step"]):
+            best = res
     if best is None:
         raise RuntimeError(f"every candidate layout failed: {times}")
+    best["config"]["autotune_ms_per_step"] = dict(times)
     return best, times
 
 
-def main():
-    args = parse()
+# ---------------------------------------------------------------------------------------------
+# runners
+# ---------------------------------------------------------------------------------------------
+
+
+class SingleRunner:
+    """One GPU, the whole graph: appnp_propagate (or its captured plan)."""
+
+    def __init__(self, graph, H, K, alpha, dtype, ld, plan=False):
+        import ppnp_amd
+
+        self.graph, self.H, self.K, self.alpha = graph, H, K, alpha
+        self.width = int(H.shape[1])
+        n = graph.n
+        self.lo, self.hi, self.f_lo, self.f_hi = 0, n, 0, self.width
+        self.Z = torch.empty(n, ld, dtype=dtype, device=H.device)[:, :self.width]
+        self.remainder_cols = graph.remainder_cols(self.width, dtype) if K >= 2 else 0
+        if plan:
+            from ppnp_amd.ops import PropagatePlan
+
+            self._plan = PropagatePlan(graph, H, K, alpha)
+            self.Z = self._plan.Z
+            self.run = self._plan
+        else:
+            self.run = lambda: ppnp_amd.propagate_forward(graph, H, K, alpha, out=self.Z)
+
+    @property
+    def out(self):
+        return self.Z
+
+
+def cand_name(cand):
+    layout, overlap, exchange = cand
+    return (f"rows{layout.rows}xcols{layout.cols}" + ("-overlap" if overlap else "")
+            + (f"-{exchange}" if (layout.rows > 1 and layout.cols > 1) or exchange == "native"
+               else ""))
+
+
+def main(argv=None):
+    args = parse(argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -235,7 +495,7 @@ def main():
         dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     if args.features:
         F = args.features
-    seed = synth.SEEDS.get(args.workload, 0)
+    dname = "bf16" if dtype == torch.bfloat16 else "f32"
     distributed = world > 1 or args.layout != "auto"
     emu = {}
     lw = world
@@ -254,14 +514,14 @@ def main():
         cands = [(layout, args.overlap, args.exchange)]
     if world > 1:
         # RCCL only where a layout has a data-path exchange (row groups); pure column layouts
-        # have none, so their control plane (barrier, max-over-ranks) runs over gloo
+        # have none, so their control plane (barrier, max-over-ranks) runs over gloo.  The
+        # process group's own watchdog (10 min) outlasts --candidate-timeout, so a stalled
+        # exchange is ended by run_candidates, which still prints a line
         rows = any(c[0].rows > 1 for c in cands)
         backend = os.environ.get("PPNP_DIST_BACKEND") or ("nccl" if rows else "gloo")
         if backend == "nccl":
-            # a collective that stalls aborts the job after 5 minutes (watchdog) instead of
-            # holding the node for the default 10
             torch.distributed.init_process_group("nccl", device_id=dev,
-                                                 timeout=datetime.timedelta(minutes=5))
+                                                 timeout=datetime.timedelta(minutes=10))
         else:
             torch.distributed.init_process_group(backend)
     # control plane (barriers, max over ranks, failure agreement) on gloo over host memory:
@@ -270,12 +530,6 @@ def main():
     if world > 1 and torch.distributed.get_backend() == "nccl":
         ctl = torch.distributed.new_group(backend="gloo")
 
-    stagger = float(os.environ.get("PPNP_BENCH_STAGGER") or 0)
-    if stagger and world > 1:
-        # rehearsals with all ranks on ONE GPU only: concurrent generation of a products-sized
-        # graph by 8 processes time-slicing one device stalls in torch.unique for minutes
-        # (0.23 s alone), so rank r starts r * stagger seconds late; never set on a real node
-        time.sleep(rank * stagger)
     t0 = time.perf_counter()
     indptr, indices = synth.graph_for(args.workload, device=dev)
     H = synth.features(n, F, dtype=dtype, device=dev)
@@ -286,245 +540,179 @@ def main():
         H = Hbuf[:, :F]
     torch.cuda.synchronize()
     t_gen = time.perf_counter() - t0
-    if rank == 0 and world > 1:
-        log(f"[bench] {args.workload}: graph and H generated in {t_gen:.2f}s")
+    if rank == 0:
+        log(f"[bench] {args.workload}: N={n} F={F} K={K} dtype={dname}: graph (host numpy "
+            f"default_rng) and H generated in {t_gen:.2f}s")
 
-    autotune = None
-    if distributed:
-        t1 = time.perf_counter()
-        if len(cands) == 1:
-            layout, overlap, exchange = cands[0]
-            runner = pdist.PartitionedAPPNP.create(indptr, indices, n, H, K, alpha, dev,
-                                                   layout=layout, overlap=overlap,
-                                                   exchange=exchange, **emu)
-        else:
-            runner, autotune = tune_layouts(cands, indptr, indices, n, H, K, alpha, dev, ctl)
-        torch.cuda.synchronize()
-        t_build = time.perf_counter() - t1
-        graph = runner.graph
-        run = runner.run
-        stream = torch.cuda.current_stream(dev)
-        F_local = runner.width
-        mine = graph.nnz_hat if runner.layout.coords(runner.rank)[1] == 0 else 0
-        nnz_t = torch.tensor([mine], dtype=torch.int64)
-        if world > 1:
-            torch.distributed.all_reduce(nnz_t, group=ctl)
-        nnz_total = int(nnz_t.item())
-    else:
-        t1 = time.perf_counter()
-        graph = ppnp_amd.Graph.from_csr(indptr, indices, None, n, mode="sym", device=dev,
-                                        features=F, dtype=dtype)
-        torch.cuda.synchronize()
-        t_build = time.perf_counter() - t1
-        Z = torch.empty(n, ld, dtype=dtype, device=dev)[:, :F]
-
-        if args.plan:
-            from ppnp_amd.ops import PropagatePlan
-
-            plan = PropagatePlan(graph, H, K, alpha)
-            Z = plan.Z
-
-            def run():
-                plan()
-        else:
-
-            def run():
-                ppnp_amd.propagate_forward(graph, H, K, alpha, out=Z)
-
-        stream = torch.cuda.current_stream(dev)
-        F_local = F
-        nnz_total = graph.nnz_hat
+    cpu_iters = K if args.cpu_iters is None else args.cpu_iters
     adj_small = None
-    if n <= 20000 and world == 1:  # the as-shipped PPNP leg of the CPU baseline needs A
+    if n <= 20000 and rank == 0:  # the as-shipped PPNP leg of the CPU baseline needs A
         import numpy as np
         import scipy.sparse as sp
 
         ip_c, ix_c = indptr.cpu().numpy(), indices.cpu().numpy()
         adj_small = sp.csr_matrix((np.ones(len(ix_c), dtype=np.float32), ix_c, ip_c),
                                   shape=(n, n))
-    if distributed:
-        ref_csr = (indptr, indices)  # rank-0 style verification of the partitioned result
-    del indices
-    if rank == 0:
-        log(f"[bench] {args.workload}: N={n} nnz_hat={nnz_total} F={F} K={K} dtype={dtype} "
-            f"gen {t_gen:.2f}s build {t_build:.3f}s"
-            + (f" layout {runner.layout}" if distributed else ""))
 
-    for _ in range(args.warmup):
-        run()
-    torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier(group=ctl)
-    torch.cuda.synchronize()
-    # one event per step boundary on the launch stream: the timed region's device time and the
-    # spread of the individual steps (reported as step_ms)
-    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
-    ev0, ev1 = evs[0], evs[-1]
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for i in range(args.steps):
-        run()
-        evs[i + 1].record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier(group=ctl)
-    torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
-    dev_ms = ev0.elapsed_time(ev1)
-    steps_ms = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps))
-    if world > 1:
-        t = torch.tensor([wall, dev_ms], dtype=torch.float64)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX, group=ctl)
-        wall, dev_ms = float(t[0]), float(t[1])
+    extras = {}  # cpu_baseline / single-GPU parity, attached to whichever line is printed
 
-    # parity of the timed result: at N > 1 every rank compares its block of Z_K with a
-    # single-GPU appnp_propagate of the whole graph on its own device (max over ranks), so a
-    # wrong exchange fails loudly instead of printing a throughput
-    dist_parity = None
-    if distributed and not args.emulate:
-        Zblk = runner.out
-        ip_r, ix_r = ref_csr
-        Gref = ppnp_amd.Graph.from_csr(ip_r, ix_r, None, n, mode="sym", device=dev)
-        Zref = ppnp_amd.propagate_forward(Gref, H, K, alpha)
-        blk = Zref[runner.lo:runner.hi, runner.f_lo:runner.f_hi]
-        err = float((Zblk.double() - blk.double()).abs().max()) if blk.numel() else 0.0
-        ref_max = float(Zref.abs().max())
-        e = torch.tensor([err, ref_max], dtype=torch.float64)
-        if world > 1:
-            torch.distributed.all_reduce(e, op=torch.distributed.ReduceOp.MAX, group=ctl)
-        err, ref_max = float(e[0]), float(e[1])
-        tol = 1e-5 * ref_max + 1e-6
-        dist_parity = {"max_abs_err": err, "tol": tol, "max_abs_ref": ref_max,
-                       "ok": err <= tol,
-                       "reference": "single-GPU appnp_propagate of the whole graph, per rank"}
-        del Gref, Zref, blk, ref_csr
-        if not dist_parity["ok"]:
-            log(f"[bench] PARITY FAILURE of the partitioned result: {dist_parity}")
-
-    s = 2 if dtype == torch.bfloat16 else 4
-    rows_local = graph.rows
-    nnz_local = graph.nnz_hat
-    # dominant kernel: one SpMM launch per iteration per rank
-    b_iter = 4 * (rows_local + 1) + 8 * nnz_local + 3 * rows_local * F_local * s
-    avg_launch_ms = dev_ms / (args.steps * K)
-    achieved = b_iter / (avg_launch_ms * 1e-3) / 1e9
-    # gather line-request rate: every nonzero gathers one row of Z_k; with
-    # split rows only the fs main columns are gathered (whole lines), the rest run the
-    # L2-blocked remainder pass (appnp_blocks.hip)
-    # (single GPU, or a column layout, whose ranks call appnp_propagate on their slab)
-    whole = not distributed or runner.layout.rows == 1
-    r_cols = graph.remainder_cols(F_local, dtype) if whole and K >= 2 else 0
-    fs = F_local - r_cols if r_cols else 0
-    ld_l = pdist.line_ld(F_local, s)
-    lines_per_row = (fs * s // 128 if r_cols else
-                     1 if ld_l * s <= 128 else -(-(F_local * s) // 128))
-    lines = nnz_local * lines_per_row + (8 * nnz_local + 3 * rows_local * ld_l * s) / 128
-    line_rate = lines / (avg_launch_ms * 1e-3) / 1e9
-    value = n * F * K * args.steps / wall
-    rows_per_s = n * K * args.steps / wall  # also N*K/t
-    parallelism = ((f"rows{runner.layout.rows}xcols{runner.layout.cols}"
-                    + ("-overlap" if runner.overlap else "")
-                    + (f"-{runner.exchange}" if (runner.layout.rows > 1 and runner.layout.cols > 1
-                       and runner.exchange != "none") or runner.exchange == "native" else "")
-                    + (f"-EMULATED-rank{args.emulate}" if args.emulate else ""))
-                   if distributed else "single")
-    traffic = committed_traffic(args.workload, dtype, parallelism)
-    res = {
-        "metric": METRIC,
-        "value": value,
-        "unit": "node-feats/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": wall * 1e3 / args.steps,
-        # device time of each timed step on this rank (HIP events): spread of the run
-        "step_ms": {"min": steps_ms[0], "median": steps_ms[len(steps_ms) // 2],
-                    "max": steps_ms[-1]},
-        "propagated_rows_per_s": rows_per_s,
-        "higher_is_better": True,
-        "scaling": "strong",
-        "vs_baseline": None,
-        "dtype": "bf16" if dtype == torch.bfloat16 else "f32",
-        "data": synth.DESCRIPTIONS.get(args.workload, "synthetic") + ", H ~ N(0,1)",
-        "config": {
-            "workload": args.workload,
-            "nodes": n,
-            "nnz_a_hat": nnz_total,
-            "F": F,
-            "K": K,
-            "alpha": alpha,
-            "norm": "sym",
-            "parallelism": parallelism,
-        },
-        "roofline": {
-            "bound": "hbm",
-            "achieved": achieved,
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS,
-            "traffic": traffic,
-            "traffic_source": "profiles/pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE / "
-                              "WRITE_SIZE passes of this bench command, gfx950-corrected)",
-            # the PMC bytes per launch over the same launch time: how fast the kernel moves
-            # the bytes the random gathers force it to move (Infinity-Cache hits included)
-            "traffic_GBs": (traffic / (avg_launch_ms * 1e-3) / 1e9) if traffic else None,
-            "traffic_frac": (traffic / (avg_launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS)
-                            if traffic else None,
-            "gather_line_rate": {
-                "lines_per_launch": lines,
-                "achieved_G_lines_s": line_rate,
-                "ceiling_G_lines_s": GATHER_LINE_CEILING,
-                "frac": line_rate / GATHER_LINE_CEILING,
-                "ceiling_source": "tools/gather_probe.hip, profiles/r1_gather_probe.txt",
-            },
-            "kernel": ("k_step_wide (one launch per iteration)" if not r_cols else
-                       ("k_rem_persist on all the slab's columns (narrow rows: one persistent "
-                        "L2-blocked launch per iteration)") if not fs else
-                       f"k_step_wide on columns [0, {fs}) of the slab + k_rem_persist (the "
-                       f"remainder columns, one persistent L2-blocked launch) per iteration; "
-                       f"times are per iteration"),
-            "bytes_per_launch": b_iter,
-            "avg_launch_ms": avg_launch_ms,
-            # the access-pattern bound: every nonzero gathers a random row of Z,
-            # i.e. `lines_per_row` 128-B line requests (3 for a split F = 100 fp32 row), plus the
-            # streamed lines, at the chip's measured random-line rate; the L2-resident remainder
-            # pass is left out, so this is a lower bound on the iteration time
-            "ceiling": {
-                "ms_per_iter": lines / (GATHER_LINE_CEILING * 1e9) * 1e3,
-                "frac": b_iter / (lines / (GATHER_LINE_CEILING * 1e9)) / 1e9 / HBM_PEAK_GBS,
-                "lines_per_nonzero": lines_per_row,
-                "basis": f"{lines:.4g} line requests per iteration at the {GATHER_LINE_CEILING} "
-                         "G lines/s random-gather rate of tools/gather_probe.hip",
-            },
-            "note": "a uniform random graph gathers whole cache lines per nonzero, so the "
-                    "compulsory-byte fraction is capped at ceiling.frac; 60 % of the "
-                    "compulsory-byte roofline is out of reach for it on one GPU",
-        },
-    }
-    if autotune is not None:
-        res["config"]["autotune_ms_per_step"] = autotune
-    if dist_parity is not None:
-        res["parity"] = dist_parity
-    cpu_iters = K if args.cpu_iters is None else args.cpu_iters
-    if world == 1 and cpu_iters > 0 and not distributed:
-        res["cpu_baseline"], Zc = cpu_baseline(graph, H, K, alpha, cpu_iters, adj_small)
-        if cpu_iters == K:
-            # value parity of the timed GPU result against the oracle's fp32 CPU loop on the
-            # same A_hat and H; fp32 bar of the tests: 1e-5 max|Z_ref| + 1e-6
-            err = float((Z.float().cpu() - Zc).abs().max())
+    def finish_cpu_baseline(graph, Zgpu, tol_bf16):
+        """rank 0, after the first timed region: the CPU baseline, and parity of the GPU Z_K of
+        the whole graph against its all-K-iterations Z_K."""
+        if rank != 0 or cpu_iters <= 0 or args.emulate:
+            return
+        cb, Zc = cpu_baseline(graph, H, K, alpha, cpu_iters, adj_small)
+        extras["cpu_baseline"] = cb
+        if cpu_iters == K and Zgpu is not None:
+            err = float((Zgpu.float().cpu() - Zc).abs().max())
             ref_max = float(Zc.abs().max())
-            tol = 1e-5 * ref_max + 1e-6
-            if dtype == torch.bfloat16:
-                tol = 2e-2 * ref_max  # bf16 storage bar
-            res["parity"] = {"max_abs_err": err, "tol": tol, "max_abs_ref": ref_max,
-                             "ok": err <= tol,
-                             "reference": "oracle fp32 torch.sparse.mm CPU loop, same A_hat "
-                                          "and H, all K iterations"}
-        del Zc
-    if rank == 0:
+            tol = 2e-2 * ref_max if tol_bf16 else 1e-5 * ref_max + 1e-6
+            extras["parity_cpu"] = {
+                "max_abs_err": err, "tol": tol, "max_abs_ref": ref_max, "ok": err <= tol,
+                "reference": "oracle fp32 torch.sparse.mm CPU loop, same A_hat and H, all K "
+                             "iterations" + ("" if world == 1 and not distributed else
+                                             "; GPU side: single-GPU appnp_propagate of the "
+                                             "whole graph on rank 0")}
+
+    def result(runner, wall, dev_ms, steps_ms, parallelism, exchange_in):
+        graph = runner.graph
+        F_local = runner.width
+        avg_iter_ms = dev_ms / (args.steps * K)
+        sb = graph.source_block_layout() if runner.remainder_cols else None
+        desc, kkey, fs, r, lpe = kernel_plan(F_local, K, runner.remainder_cols, sb)
+        tkey = traffic_key(args.workload, dname, parallelism, kkey)
+        rl = roofline(n=n, rows=graph.rows, nnz=graph.nnz_hat, F_local=F_local, esz=esz,
+                      avg_iter_ms=avg_iter_ms, fs=fs, r=r, lpe=lpe,
+                      rb_total=sb["entries"] if r else 0,
+                      rb_entry_bytes=4 if (r and sb["value_free"]) else 8,
+                      exchange_in_bytes=exchange_in, kernel=desc, kernel_key=kkey,
+                      traffic=committed_traffic(tkey))
+        rl["traffic_key"] = tkey
+        return {
+            "metric": METRIC,
+            "value": n * F * K * args.steps / wall,
+            "unit": "node-feats/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": wall * 1e3 / args.steps,
+            # device time of each timed step on this rank (HIP events): spread of the run
+            "step_ms": {"min": steps_ms[0], "median": steps_ms[len(steps_ms) // 2],
+                        "max": steps_ms[-1]},
+            "propagated_rows_per_s": n * K * args.steps / wall,  # SURVEY 8(d): also N*K/t
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": dname,
+            "data": synth.DESCRIPTIONS.get(args.workload, "synthetic") + ", H ~ N(0,1)",
+            "config": {
+                "workload": args.workload,
+                "nodes": n,
+                "nnz_a_hat": None,  # filled by the caller (whole graph)
+                "F": F,
+                "K": K,
+                "alpha": alpha,
+                "norm": "sym",
+                "parallelism": parallelism,
+            },
+            "roofline": rl,
+        }
+
+    stream = torch.cuda.current_stream(dev)
+    if not distributed:
+        t1 = time.perf_counter()
+        graph = ppnp_amd.Graph.from_csr(indptr, indices, None, n, mode="sym", device=dev,
+                                        features=F, dtype=dtype)
+        torch.cuda.synchronize()
+        t_build = time.perf_counter() - t1
+        del indices
+        runner = SingleRunner(graph, H, K, alpha, dtype, ld, plan=args.plan)
+        log(f"[bench] nnz_hat={graph.nnz_hat} build {t_build:.3f}s")
+        wall, dev_ms, steps_ms = time_steps(runner.run, stream, args.steps, args.warmup, 1, None)
+        res = result(runner, wall, dev_ms, steps_ms, "single", 0)
+        res["config"]["nnz_a_hat"] = graph.nnz_hat
+        finish_cpu_baseline(graph, runner.out, dtype == torch.bfloat16)
+        if "cpu_baseline" in extras:
+            res["cpu_baseline"] = extras["cpu_baseline"]
+        if "parity_cpu" in extras:
+            res["parity"] = extras["parity_cpu"]
         print(json.dumps(res), flush=True)
+        return res
+
+    # -- partitioned: every rank's reference is a single-GPU propagation of the whole graph ---
+    Gref = ppnp_amd.Graph.from_csr(indptr, indices, None, n, mode="sym", device=dev)
+    Zref = ppnp_amd.propagate_forward(Gref, H, K, alpha) if not args.emulate else None
+    nnz_total = Gref.nnz_hat
+    ref_max = float(Zref.abs().max()) if Zref is not None else 0.0
+    tol = (2e-2 * ref_max) if dtype == torch.bfloat16 else 1e-5 * ref_max + 1e-6
+    first_timed = [True]
+
+    def measure(cand):
+        layout, overlap, exchange = cand
+        t1 = time.perf_counter()
+        runner = pdist.PartitionedAPPNP.create(indptr, indices, n, H, K, alpha, dev,
+                                               layout=layout, overlap=overlap,
+                                               exchange=exchange, **emu)
+        torch.cuda.synchronize()
+        t_build = time.perf_counter() - t1
+        try:
+            wall, dev_ms, steps_ms = time_steps(runner.run, stream, args.steps, args.warmup,
+                                                world, ctl)
+            par = (cand_name(cand) if not args.emulate else
+                   cand_name(cand) + f"-EMULATED-rank{args.emulate}")
+            R = runner.layout.rows
+            # the other row shards of this rank's column group land here every iteration
+            exchange_in = ((R - 1) * runner.shard * runner.width * esz
+                           if R > 1 and not args.emulate else 0)
+            res = result(runner, wall, dev_ms, steps_ms, par, exchange_in)
+            res["config"]["nnz_a_hat"] = nnz_total
+            res["config"]["build_s"] = t_build
+            if Zref is not None:
+                blk = Zref[runner.lo:runner.hi, runner.f_lo:runner.f_hi]
+                err = (float((runner.out.double() - blk.double()).abs().max())
+                       if blk.numel() else 0.0)
+                e = torch.tensor([err], dtype=torch.float64)
+                if world > 1:
+                    torch.distributed.all_reduce(e, op=torch.distributed.ReduceOp.MAX,
+                                                 group=ctl)
+                err = float(e[0])
+                res["parity"] = {"max_abs_err": err, "tol": tol, "max_abs_ref": ref_max,
+                                 "ok": err <= tol,
+                                 "reference": "single-GPU appnp_propagate of the whole graph, "
+                                              "per rank (max over ranks)"}
+            if first_timed[0]:
+                first_timed[0] = False
+                # the CPU baseline once, after the first (exchange-free) timed region, so a
+                # later candidate's stall cannot lose it
+                try:
+                    finish_cpu_baseline(Gref, Zref, dtype == torch.bfloat16)
+                except Exception as e:  # noqa: BLE001 -- a baseline, not the candidate
+                    log(f"[bench] cpu_baseline failed: {type(e).__name__}: {e}")
+                if world > 1:
+                    torch.distributed.barrier(group=ctl)
+            return res
+        finally:
+            del runner
+            torch.cuda.empty_cache()
+
+    def emit(res):
+        for k in ("cpu_baseline", "parity_cpu"):
+            if k in extras:
+                res[k] = extras[k]
+        print(json.dumps(res), flush=True)
+
+    if len(cands) == 1:
+        res = measure(cands[0])
+        if args.layout == "auto":
+            res["config"]["autotune_ms_per_step"] = {cand_name(cands[0]): res["ms_per_step"]}
+    else:
+        res, _ = run_candidates(cands, measure, ctl, args.candidate_timeout, emit, cand_name,
+                                rank, world)
+    if rank == 0:
+        emit(res)
     if world > 1:
         torch.distributed.destroy_process_group()
+    return res
 
 
 if __name__ == "__main__":

@@ -172,21 +172,33 @@ int appnp_graph_source_blocks(const appnp_graph* g, int64_t* bytes);
 int appnp_graph_dinv(const appnp_graph* g, const double** dinv);
 
 /* Bytes of workspace appnp_propagate / appnp_propagate_bwd need for this shape.  The
- * workspace holds the ping-pong iterates with its own line-aligned leading dimension
- * (`ld` is accepted for ABI stability and ignored). */
+ * workspace holds the ping-pong iterates with its own line-aligned leading dimension, or the
+ * two buffers of the split layout ([n, fs] + [n, width of the source-blocked copy]), whichever
+ * is larger (`ld` is accepted for ABI stability and ignored). */
 size_t appnp_workspace_bytes(const appnp_graph* g, int64_t f, int64_t ld, int dtype);
 
-/* The column split appnp_propagate uses for this shape when H, Z and the workspace are 16-B
- * aligned with leading dimensions that are multiples of 4 (K >= 2): *fs = 32q for fp32 rows of
- * F = 32q + r features, 1 <= r <= 4, on a graph built with APPNP_GRAPH_SOURCE_BLOCKS (then
- * columns [0, fs) gather whole cache lines and [fs, F) run the L2-blocked remainder pass);
- * *fs = 0 when rows are gathered whole.  Informational: appnp_propagate decides by itself. */
+/* The column split appnp_propagate uses for this shape when H and Z are 16-B aligned with
+ * leading dimensions that are multiples of 4 floats (K >= 2): columns [0, *fs) gather whole cache
+ * lines and [*fs, F) run the persistent L2-blocked remainder pass.  fp32 rows of F = 32q + r
+ * features take it on a graph built with a source-blocked copy, above 2^16 nodes and without
+ * gather locality: r <= 4 on an APPNP_GRAPH_SOURCE_BLOCKS copy, r <= 8 on an APPNP_GRAPH_SB_W8 /
+ * _W16 copy (wider remainders beside a main part keep whole rows).  *fs = 0 when rows are
+ * gathered whole, and also for narrow rows, which run wholly in the pass (see below).
+ * Informational: appnp_propagate decides by itself, on the same rule. */
 int appnp_propagate_split_point(const appnp_graph* g, int64_t f, int dtype, int64_t* fs);
 
-/* The remainder columns of that split: *r = F - fs columns run the L2-blocked pass (1-4, or
- * up to 8 on a graph built with APPNP_GRAPH_SB_W8 / _W16, where narrow rows F <= 8 / 16 run
- * wholly in the pass, with *fs = 0); *r = 0 when rows are gathered whole. */
+/* The remainder columns of that split: *r = F - fs columns run the L2-blocked pass -- 1-4 on an
+ * APPNP_GRAPH_SOURCE_BLOCKS copy, up to 8 on a W8 / W16 copy -- and narrow rows F <= 4 / 8 / 16
+ * (the copy's width) run wholly in the pass, *r = F with *fs = 0.  *r = 0 when rows are
+ * gathered whole. */
 int appnp_propagate_remainder_cols(const appnp_graph* g, int64_t f, int dtype, int64_t* r);
+
+/* The source-blocked copy as built: *width remainder columns per row (4, 8, 16; 0 = not built),
+ * *entries regrouped entries including padding, *value_free = 1 when entries carry no values
+ * (unit graph: A_hat_ij = dl_i dr_j), *row_passes row-group passes per launch, and *launches the
+ * remainder-pass launches enqueued on this graph so far (which path a propagation took). */
+int appnp_graph_source_block_layout(const appnp_graph* g, int* width, int64_t* entries,
+                                    int* value_free, int* row_passes, int64_t* launches);
 
 /*
  * Z = APPNP_K(H):  Z_0 = H;  Z_{k+1} = (1-alpha) (M_k o A_hat) Z_k + alpha H,  k < K.
@@ -195,11 +207,11 @@ int appnp_propagate_remainder_cols(const appnp_graph* g, int64_t f, int dtype, i
  *   hash of (seed, k, i, j) >= p_drop * 2^24, and scales kept edges by 1/(1-p_drop).
  *   p_drop = 0 is eval mode (the reference's semantics).
  *   ws: appnp_workspace_bytes() bytes (may be NULL when that is 0).
- * One fused kernel launch per iteration.  With split rows (appnp_propagate_split_point > 0)
- * an iteration is that launch on the first fs columns plus the remainder pass (one launch per
- * source block), and H is first copied into the workspace's split layout.  All launches are
- * stream-ordered on `stream`; nothing is allocated or synchronised.  Requires a full
- * (non-partitioned) graph.
+ * One fused kernel launch per iteration.  With split rows (appnp_propagate_remainder_cols >
+ * 0) an iteration is that launch on the first fs columns (none for narrow rows) plus ONE
+ * persistent launch of the L2-blocked remainder pass over every source block, and H is first
+ * copied into the workspace's split layout.  All launches are stream-ordered on `stream`;
+ * nothing is allocated or synchronised.  Requires a full (non-partitioned) graph.
  */
 int appnp_propagate(const appnp_graph* g, const void* H, int64_t ld_h, void* Z, int64_t ld_z,
                     int64_t f, int dtype, int K, float alpha, float p_drop, uint64_t seed,
@@ -231,6 +243,39 @@ int appnp_step(const appnp_graph* g, int part, const void* Zin, int64_t ld_in, c
                int64_t ld_h, void* Zout, int64_t ld_out, const float* partial,
                int64_t ld_partial, int64_t f, int dtype, int k, float alpha, float p_drop,
                uint64_t seed, void* stream);
+
+/*
+ * Split rows on the held rows of a row-partitioned graph (appnp_graph_create_rows with a
+ * source-blocked copy, APPNP_GRAPH_SOURCE_BLOCKS / _SB_W8 / _SB_W16; fp32; the split rule of
+ * appnp_propagate_remainder_cols).  The iterate is kept as two FULL-HEIGHT parts (every rank's
+ * rows, global row index): main [rows_total, fs] (fs = F - r columns, whole cache lines per
+ * gathered row) and rem [rows_total, rem_width] (the r remainder columns, zero padded; on a unit
+ * graph scaled by the column scale of A_hat, which only these functions read and write).  Each
+ * rank writes its held rows of both parts; an exchange (all-gather) fills the others.  All
+ * buffers 16-B aligned, leading dimensions multiples of 4 floats.
+ *
+ * appnp_split_layout  *fs and *rem_width of that layout for F; APPNP_ENOTSUP when F does not
+ *                     split on this graph (then use appnp_step).
+ * appnp_split_copy    the held rows of H (ld_h) into rows [row_lo, row_hi) of main and rem: the
+ *                     Z_0 parts.  main may be NULL when fs = 0.
+ * appnp_step_split    one iteration of the held rows from all rows of zin_main / zin_rem:
+ *                     into rows [row_lo, row_hi) of zout_main / zout_rem, or, when Z != NULL,
+ *                     into the held rows of Z (ld_z, all F columns: the last iteration).  part
+ *                     as for appnp_step, on the main columns: ALL (then the remainder pass),
+ *                     LOCAL (local-column product of the main part into the fp32 `partial`
+ *                     [held rows, fs], ld_partial; zin_rem is not read, so it may still be in
+ *                     flight), REMOTE (remote columns + partial + alpha H, then the remainder
+ *                     pass).  LOCAL / REMOTE need split_local.  Stream-ordered, no allocation.
+ * the north_star's row partition gathers q lines per nonzero for F = 32q + r
+ * instead of q + 1, as the single-GPU appnp_propagate does.
+ */
+int appnp_split_layout(const appnp_graph* g, int64_t f, int64_t* fs, int64_t* rem_width);
+int appnp_split_copy(const appnp_graph* g, const float* H, int64_t ld_h, int64_t f, float* main,
+                     float* rem, void* stream);
+int appnp_step_split(const appnp_graph* g, int part, const float* zin_main, const float* zin_rem,
+                     const float* H, int64_t ld_h, float* zout_main, float* zout_rem, float* Z,
+                     int64_t ld_z, float* partial, int64_t ld_partial, int64_t f, int k,
+                     float alpha, float p_drop, uint64_t seed, void* stream);
 
 /*
  * A captured propagation plan: the K launches of appnp_propagate for FIXED buffers (H, Z, ws)
@@ -270,8 +315,12 @@ typedef int (*appnp_allgather_fn)(void* buf, size_t shard_bytes, int rank, int n
                                   void* stream, void* ctx);
 
 /* indptr/indices/vals/n/nnz/mode: the WHOLE graph's A on this device, as appnp_graph_create.
+ * `mode` may carry APPNP_GRAPH_SOURCE_BLOCKS / _SB_W8 / _SB_W16: then fp32 propagations whose
+ * F splits (appnp_split_layout) with 16-B aligned H / Z run on the split layout (main part
+ * gathers whole lines, remainder pass; appnp_step_split).
  * overlap != 0 keeps the held rows as local- and remote-column CSRs (fp32 propagation only).
- * allgather/ctx: the exchange, called once per exchanged iterate by every rank. */
+ * allgather/ctx: the exchange, called by every rank once per exchanged iterate (twice on the
+ * split layout: its main part, then its remainder part). */
 int appnp_dist_create(const int32_t* indptr, const int32_t* indices, const float* vals,
                       int64_t n, int64_t nnz, int mode, int rank, int nranks, int overlap,
                       appnp_allgather_fn allgather, void* ctx, void* stream, appnp_dist** out);
@@ -280,8 +329,9 @@ int appnp_dist_create(const int32_t* indptr, const int32_t* indices, const float
 int appnp_dist_rows(const appnp_dist* d, int64_t* row_lo, int64_t* row_hi, int64_t* shard);
 const appnp_graph* appnp_dist_graph(const appnp_dist* d);
 
-/* Workspace of appnp_dist_propagate: two full-height iterates (P S rows, line-aligned) and, with
- * overlap, the fp32 local-column partial of the held rows. */
+/* Workspace of appnp_dist_propagate: two full-height iterates (P S rows, line-aligned, or the
+ * two parts of the split layout) and, with overlap, the fp32 local-column partial of the held
+ * rows; the larger of the two layouts when F splits. */
 size_t appnp_dist_workspace_bytes(const appnp_dist* d, int64_t f, int dtype);
 
 /*

@@ -54,6 +54,9 @@ _SIGS = {
     "appnp_propagate_split_point": (_i32, [_vp, _i64, _i32, C.POINTER(_i64)]),
     "appnp_propagate_remainder_cols": (_i32, [_vp, _i64, _i32, C.POINTER(_i64)]),
     "appnp_graph_source_blocks": (_i32, [_vp, C.POINTER(_i64)]),
+    "appnp_graph_source_block_layout": (_i32, [_vp, C.POINTER(_i32), C.POINTER(_i64),
+                                               C.POINTER(_i32), C.POINTER(_i32),
+                                               C.POINTER(_i64)]),
     "appnp_propagate": (
         _i32,
         [_vp, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _f32, _f32, _u64, _vp, _sz, _vp],
@@ -95,6 +98,13 @@ _SIGS = {
     "appnp_step": (
         _i32,
         [_vp, _i32, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _f32,
+         _f32, _u64, _vp],
+    ),
+    "appnp_split_layout": (_i32, [_vp, _i64, C.POINTER(_i64), C.POINTER(_i64)]),
+    "appnp_split_copy": (_i32, [_vp, _vp, _i64, _i64, _vp, _vp, _vp]),
+    "appnp_step_split": (
+        _i32,
+        [_vp, _i32, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _i64, _vp, _i64, _i64, _i32, _f32,
          _f32, _u64, _vp],
     ),
 }

@@ -31,15 +31,18 @@
 // lane, sorted by (row, column); gathers Z_rem[column] from L2; and combines the products
 // of equal rows with a segmented inclusive scan over the lanes (DPP row shifts + row
 // broadcasts, fixed order); each segment's last lane adds the sum into its row's LDS slot.
-// U = 8 chunks (512 entries) are in flight per wave: the pass is bound by the latency of the
-// entry load followed by the dependent L2 gather, not by bandwidth.  The order of every
-// addition is fixed by the layout: bitwise deterministic run to run.
+// U = 2 chunks (128 entries; APPNP_REM_U at compile time) are in flight per wave: fewer chunks
+// keep the waves of an XCD close together in the block sweep, so fewer blocks share its L2
+// (92 % hits at U = 2, 66 % at U = 8).  The order of every addition is fixed by
+// the layout: bitwise deterministic run to run.
 //
-// The regrouped copy of A_hat (APPNP_GRAPH_SOURCE_BLOCKS) is built at graph creation: the
-// entries of wave group g's block b are the segment off[g * nb + b] .. off[g * nb + b + 1],
-// packed as (row in group << 20 | column in block) with their fp32 value; padding entries are
-// all ones with value 0.  off holds passes x (CUs x 16) x blocks + 1 ints: linear in n
-// (one int per 640-row x 2^15-column tile of A_hat, ~1.2 MB on products-synth).
+// The regrouped copy of A_hat (APPNP_GRAPH_SOURCE_BLOCKS / _SB_W8 / _SB_W16) is built at graph
+// creation: the entries of wave group g's block b are the segment off[g * nb + b] ..
+// off[g * nb + b + 1], each packed into 32 bits as (row in group << kRemColBits | column in
+// block), kRemColBits = 20, with their fp32 value (none on a unit graph, below); padding
+// entries are kRemNone (all ones) with value 0.  A wave group holds 640 / LPE rows.  off holds
+// passes x (CUs x 16) x blocks + 1 ints: linear in n (one int per (640 / LPE)-row x 2^15-column
+// tile of A_hat, ~1.2 MB on products-synth at LPE = 1).
 //
 // A unit graph (unweighted A without self loops: every entry of A+I is 1, so A_hat_ij =
 // dl_i dr_j with sym: dl = dr = dinv, rw: dl = dinv, dr = 1) stores NO values: the remainder
@@ -83,9 +86,10 @@ struct RemLayout {
   const uint32_t* ent;  // packed (row in group, column in block); padding: kRemNone
   const float* val;     // entry values; null for a unit graph (VF kernels)
   const int32_t* cblk;  // source block of each chunk of 64 entries
-  const float* dl;      // VF: row scale of A_hat (fp32 dinv)
-  const float* dr;      // VF: column scale (sym: fp32 dinv; rw: null).  Z_rem buffers hold
-                        // dr o Z_rem, so a gathered row needs no value
+  const float* dl;      // VF: row scale of A_hat (fp32 dinv) of the held rows (local index)
+  const float* dr;      // VF: column scale (sym: fp32 dinv; rw: null) of all n rows (global
+                        // index).  Z_rem buffers hold dr o Z_rem, so a gathered row needs no
+                        // value
   int32_t nb, br_log2, slots, rg, passes;
   int32_t scale_out;    // VF: the output is the next remainder buffer (store dr o y)
 };
@@ -165,7 +169,7 @@ __device__ __forceinline__ void rem_finish(const StepArgs& a, const RemLayout& L
   if constexpr (VF) {
     const float dl = L.dl[i];
     acc = f32x4{dl * acc.x, dl * acc.y, dl * acc.z, dl * acc.w};
-    if (L.scale_out && L.dr) so = L.dr[i];
+    if (L.scale_out && L.dr) so = L.dr[a.row_lo + i];  // dr: all n rows (global index)
   }
   if constexpr (EPI == EPI_BWD) {
     const float y[4] = {a.scale * acc.x, a.scale * acc.y, a.scale * acc.z, a.scale * acc.w};
@@ -220,7 +224,7 @@ __device__ __forceinline__ void rem_finish_piece(const StepArgs& a, const RemLay
   if constexpr (VF) {
     const float dl = L.dl[i];
     acc = f32x4{dl * acc.x, dl * acc.y, dl * acc.z, dl * acc.w};
-    if (L.scale_out && L.dr) so = L.dr[i];
+    if (L.scale_out && L.dr) so = L.dr[a.row_lo + i];
   }
   float y[4] = {a.scale * acc.x, a.scale * acc.y, a.scale * acc.z, a.scale * acc.w};
   if constexpr (EPI == EPI_BWD) {
@@ -289,8 +293,11 @@ __global__ __launch_bounds__(kRemThreads) void k_rem_persist(StepArgs a, RemLayo
           zv[u] = en[u] != kRemNone ? z[cb[u] + (int32_t)(en[u] & cmask)]
                                     : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
         } else {
-          zv[u] = en[u] != kRemNone ? z[(int64_t)(cb[u] + (int32_t)(en[u] & cmask)) * LPE + q]
-                                    : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+          // a piece wholly past the valid remainder columns (a.f) holds zeros in every buffer:
+          // no request for it (a 4-column remainder on a W8 / W16 copy gathers one piece)
+          zv[u] = (en[u] != kRemNone && 4 * q < a.f)
+                      ? z[(int64_t)(cb[u] + (int32_t)(en[u] & cmask)) * LPE + q]
+                      : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
         }
       }
 #pragma unroll
@@ -302,8 +309,9 @@ __global__ __launch_bounds__(kRemThreads) void k_rem_persist(StepArgs a, RemLayo
         const int key = LPE == 1 ? row : ((row << 3) | q);
         f32x4 v = zv[u];
         if (!VF || a.drop_on) {
-          const float w =
-              act ? edge_weight(wt[u], r0 + row, cb[u] + (int32_t)(en[u] & cmask), a) : 0.0f;
+          const float w = act ? edge_weight(wt[u], a.row_lo + r0 + row,
+                                            cb[u] + (int32_t)(en[u] & cmask), a)
+                              : 0.0f;
           v = f32x4{w * v.x, w * v.y, w * v.z, w * v.w};
         }
         // the previous lane's row (lane 0: none), by DPP rather than an LDS permute
@@ -336,7 +344,8 @@ template <bool FILL>
 __global__ __launch_bounds__(kBlock) void k_rb_walk(const int32_t* __restrict__ rp,
                                                     const int32_t* __restrict__ col,
                                                     const float* __restrict__ val, int64_t n,
-                                                    int rg, int nb, int br_log2, int chunk,
+                                                    int64_t row_lo, int rg, int nb, int br_log2,
+                                                    int chunk,
                                                     int64_t n_groups, int32_t* __restrict__ cnt,
                                                     const int32_t* __restrict__ off,
                                                     uint32_t* __restrict__ ent,
@@ -373,7 +382,7 @@ __global__ __launch_bounds__(kBlock) void k_rb_walk(const int32_t* __restrict__ 
           if (bval) bval[pos] = val[e];
         }
       } else {
-        const int64_t d = (int64_t)c - i;
+        const int64_t d = (int64_t)c - (row_lo + i);  // global row vs global column
         nr += (act && d != 0 && d < kNearRows && d > -kNearRows) ? 1 : 0;
       }
       if (tail) cur[b] = base + (lane - head + 1);
@@ -482,8 +491,8 @@ int env_or(const char* name, int dflt) {
 // (appnp_graph_create_rows): APPNP_ENOTSUP / APPNP_ERANGE / APPNP_ENOMEM leave the graph
 // without it, and appnp_propagate gathers whole rows.
 int graph_build_source_blocks(appnp_graph* g, int lpe, hipStream_t s) {
+  // the held rows [row_lo, row_hi) in row groups; source blocks over all n global columns
   const int64_t rows = g->row_hi - g->row_lo;
-  if (g->row_lo != 0 || rows != g->n) return APPNP_EINVAL;
   if (lpe != 1 && lpe != 2 && lpe != 4) return APPNP_EINVAL;
   const int chunk = kRemChunk / lpe;     // entries per chunk (one per lpe lanes)
   const int max_rg = kRemMaxRg / lpe;    // rows per wave group: 16 x max_rg x 16 lpe B of LDS
@@ -532,7 +541,8 @@ int graph_build_source_blocks(appnp_graph* g, int lpe, hipStream_t s) {
       ok(hipMalloc(&tot, 2 * sizeof(int64_t))) &&
       ok(hipMemsetAsync(tot, 0, 2 * sizeof(int64_t), s))) {
     hipLaunchKernelGGL(k_rb_walk<false>, dim3(grid), dim3(kBlock), lds, s, g->row_ptr, g->col,
-                       g->val, rows, (int)rg, (int)nb, br_log2, chunk, n_groups, cnt, nullptr,
+                       g->val, rows, g->row_lo, (int)rg, (int)nb, br_log2, chunk, n_groups, cnt,
+                       nullptr,
                        nullptr,
                        nullptr, reinterpret_cast<unsigned long long*>(tot + 1));
     if (ok(hipGetLastError()) && ok(exclusive_scan(cnt, cells, g->rb_off, bsum, tot, s)) &&
@@ -542,22 +552,31 @@ int graph_build_source_blocks(appnp_graph* g, int lpe, hipStream_t s) {
       if (h_tot[0] > INT32_MAX) rc = APPNP_ERANGE;
     }
     const int64_t total = std::max<int64_t>(1, h_tot[0]);
-    if (rc == APPNP_OK && ok(hipMalloc(&g->rb_ent, total * sizeof(uint32_t))) &&
+    // APPNP_SB_TEST_OOM (tests): ask for an impossible size, so the best-effort ENOMEM path
+    // runs with a real failing hipMalloc
+    const size_t ent_bytes = env_or("APPNP_SB_TEST_OOM", 0) ? (size_t)1 << 60
+                                                            : (size_t)total * sizeof(uint32_t);
+    if (rc == APPNP_OK && ok(hipMalloc(&g->rb_ent, ent_bytes)) &&
         (vf || ok(hipMalloc(&g->rb_val, total * sizeof(float)))) &&
         ok(hipMemsetAsync(g->rb_ent, 0xff, total * sizeof(uint32_t), s)) &&  // kRemNone
         (vf || ok(hipMemsetAsync(g->rb_val, 0, total * sizeof(float), s))) &&
-        (!vf || ok(hipMalloc(&g->rb_dl, rows * sizeof(float)))) &&
-        (!vf || g->mode != APPNP_NORM_SYM || ok(hipMalloc(&g->rb_dr, rows * sizeof(float)))) &&
+        (!vf || ok(hipMalloc(&g->rb_dl, std::max<int64_t>(1, rows) * sizeof(float)))) &&
+        (!vf || g->mode != APPNP_NORM_SYM ||
+         ok(hipMalloc(&g->rb_dr, std::max<int64_t>(1, g->n) * sizeof(float)))) &&
         ok(hipMalloc(&g->rb_cblk, std::max<int64_t>(1, total / chunk) * sizeof(int32_t)))) {
       hipLaunchKernelGGL(k_rb_walk<true>, dim3(grid), dim3(kBlock), lds, s, g->row_ptr, g->col,
-                         g->val, rows, (int)rg, (int)nb, br_log2, chunk, n_groups, nullptr,
+                         g->val, rows, g->row_lo, (int)rg, (int)nb, br_log2, chunk, n_groups,
+                         nullptr,
                          g->rb_off,
                          g->rb_ent, g->rb_val, nullptr);
       if (vf && ok(hipGetLastError())) {
-        const unsigned gb = (unsigned)((rows + kBlock - 1) / kBlock);
-        hipLaunchKernelGGL(k_dinv_f32, dim3(gb), dim3(kBlock), 0, s, g->dinv, rows, g->rb_dl);
-        if (g->rb_dr)
-          hipLaunchKernelGGL(k_dinv_f32, dim3(gb), dim3(kBlock), 0, s, g->dinv, rows, g->rb_dr);
+        // dl: the held rows' scale (local index); dr: every column's (global index)
+        if (rows > 0)
+          hipLaunchKernelGGL(k_dinv_f32, dim3((unsigned)((rows + kBlock - 1) / kBlock)),
+                             dim3(kBlock), 0, s, g->dinv + g->row_lo, rows, g->rb_dl);
+        if (g->rb_dr && g->n > 0)
+          hipLaunchKernelGGL(k_dinv_f32, dim3((unsigned)((g->n + kBlock - 1) / kBlock)),
+                             dim3(kBlock), 0, s, g->dinv, g->n, g->rb_dr);
       }
       if (ok(hipGetLastError()))
         hipLaunchKernelGGL(k_rb_chunks, dim3((unsigned)((cells + kBlock - 1) / kBlock)),
@@ -570,6 +589,10 @@ int graph_build_source_blocks(appnp_graph* g, int lpe, hipStream_t s) {
   if (bsum) (void)hipFree(bsum);
   if (tot) (void)hipFree(tot);
   if (rc != APPNP_OK) {
+    // the graph stays usable without the copy: clear the failed call's error from this
+    // thread's last-error slot, or the next hipGetLastError (a launch check here or in the
+    // caller's framework) would report it as its own
+    (void)hipGetLastError();
     if (g->rb_off) (void)hipFree(g->rb_off);
     if (g->rb_ent) (void)hipFree(g->rb_ent);
     if (g->rb_val) (void)hipFree(g->rb_val);

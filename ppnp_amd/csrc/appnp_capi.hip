@@ -3,6 +3,7 @@
 // Argument validation, workspace ping-pong and the K-iteration launch sequence.  No host
 // synchronisation or allocation happens in appnp_propagate / appnp_propagate_bwd /
 // appnp_step, so a caller may capture them in a hipGraph.
+#include <algorithm>
 #include <cstdlib>
 #include <new>
 
@@ -80,18 +81,28 @@ int env_flag(const char* name, int dflt) {
   return (v && *v) ? atoi(v) : dflt;
 }
 
-// Split rows (appnp_blocks.hip): fp32 rows of F = 32q + r features, 1 <= r <= 4, gather q whole
-// lines from the split layout [n, 32q]; the r remainder columns run as a separate chain of
-// L2-resident passes over the source-blocked A_hat.  Returns the split point 32q, or 0 when the path does
-// not apply (no blocked copy, bf16, latency-regime graph, F outside (32, 256], vectors
-// narrower than 16 B).  APPNP_SPLIT=0 disables it (measurement).
-// Remainder columns r of the split for this shape (0: rows gathered whole); the main part is
-// f - r columns (a multiple of 32, possibly 0).  r <= 4 rb_lpe: 1-4 columns on a graph built
-// with APPNP_GRAPH_SOURCE_BLOCKS, up to 8 / 16 with APPNP_GRAPH_SB_W8 / _W16, and narrow rows
-// (f <= 4 rb_lpe) run wholly in the remainder pass.
-int64_t remainder_cols(const appnp_graph* g, int64_t f, int dtype, int V) {
+// Whether every operand allows 16-B vectors: leading dimensions multiples of 4 floats and
+// 16-B aligned base pointers (null pointers ignored).  The split path reads and writes H / Z
+// (dZ / dH) in 16-B pieces: the split copy, the main kernel at V = 4 and the remainder epilogue.
+bool vec16(const int64_t* lds, int n_ld, const void* const* ptrs, int n_ptr) {
+  for (int i = 0; i < n_ld; ++i)
+    if (lds[i] % 4) return false;
+  for (int i = 0; i < n_ptr; ++i)
+    if (ptrs[i] && (reinterpret_cast<uintptr_t>(ptrs[i]) % 16)) return false;
+  return true;
+}
+
+// Split rows (appnp_blocks.hip): the remainder columns r of fp32 rows of F = 32q + r features run
+// as a separate chain of persistent L2-resident passes over the source-blocked A_hat, and the
+// main part f - r (a multiple of 32, possibly 0) gathers whole lines from the split layout
+// [n, 32q].  r <= 4 rb_lpe: 1-4 columns on a graph built with APPNP_GRAPH_SOURCE_BLOCKS, up to
+// 8 / 16 with APPNP_GRAPH_SB_W8 / _W16; narrow rows (f <= 4 rb_lpe) run wholly in the pass.
+// Returns 0 (rows gathered whole) when the path does not apply: no blocked copy, bf16,
+// latency-regime graph, F outside [1, 256], operands that do not allow 16-B vectors
+// (``aligned``), or a graph with gather locality.  APPNP_SPLIT=0 disables it (measurement).
+int64_t remainder_cols(const appnp_graph* g, int64_t f, int dtype, bool aligned) {
   static const int enabled = env_flag("APPNP_SPLIT", 1);
-  if (!enabled || !g->rb_off || dtype != APPNP_F32 || V != 4) return 0;
+  if (!enabled || !g->rb_off || dtype != APPNP_F32 || !aligned) return 0;
   if (g->n <= (1 << 16) || f < 1 || f > 256) return 0;
   // graphs with gather locality keep whole rows: their last line is mostly an L2 hit, cheaper
   // than the remainder pass (products-local, ~90 % near entries: 4.0 ms whole rows, 3.7 ms for
@@ -108,9 +119,16 @@ int64_t remainder_cols(const appnp_graph* g, int64_t f, int dtype, int V) {
 }
 
 // the main part of the split (columns [0, fs)), 0 when there is no split or no main part
-int64_t split_point(const appnp_graph* g, int64_t f, int dtype, int V) {
-  const int64_t r = remainder_cols(g, f, dtype, V);
+int64_t split_point(const appnp_graph* g, int64_t f, int dtype, bool aligned) {
+  const int64_t r = remainder_cols(g, f, dtype, aligned);
   return r ? f - r : 0;
+}
+
+// Bytes of the two split buffers ([n, fs] + [n, 4 rb_lpe] fp32 each, 256-B aligned)
+inline void split_sizes(const appnp_graph* g, int64_t n, int64_t fs, int64_t* main_b,
+                        int64_t* buf_b) {
+  *main_b = (n * fs * 4 + 255) / 256 * 256;
+  *buf_b = (*main_b + n * 16 * g->rb_lpe + 255) / 256 * 256;
 }
 
 // The forward loop in the split layout (appnp_blocks.hip).  Propagation is column-separable,
@@ -136,6 +154,7 @@ int propagate_split(const appnp_graph* g, const StepArgs& a0, const void* H, int
   float* z = static_cast<float*>(Z);
   int rc = dev_err(appnp::launch_split_copy(h, ld_h, n, f, fs, rw, main_of(0), rem_of(0),
                                             appnp::remainder_scale(g), s));
+  g->rem_launches.fetch_add(K, std::memory_order_relaxed);
   StepArgs am = a0, ar = a0;  // main / remainder chain
   am.f = (int32_t)fs;
   am.h = H;
@@ -178,6 +197,7 @@ int propagate_bwd_split(const appnp_graph* g, const StepArgs& a0, const void* dZ
   int rc = dev_err(appnp::launch_split_copy(static_cast<const float*>(dZ), ld_dz, n, f, fs, rw,
                                             main_of(0), rem_of(0), appnp::remainder_scale(g),
                                             s));
+  g->rem_launches.fetch_add(K, std::memory_order_relaxed);
   StepArgs am = a0, ar = a0;  // main / remainder chain
   am.f = (int32_t)fs;
   am.aux = dH;
@@ -248,10 +268,11 @@ int appnp_graph_create_rows(const int32_t* indptr, const int32_t* indices, const
   // A_hat^T for the adjoint, unless A_hat is symmetric already ('sym' on undirected A)
   if (rc == APPNP_OK && want_t && !(g->mode == APPNP_NORM_SYM && g->symmetric))
     rc = appnp::graph_build_transpose(g, as_stream(stream));
-  // source-blocked copy for the remainder pass (full graphs; appnp_propagate uses it).
-  // Best-effort: a graph too large for the copy (block or segment count, device memory) keeps
-  // whole-row gathers -- appnp_graph_source_blocks reports whether it was built.
-  if (rc == APPNP_OK && want_sb && row_lo == 0 && row_hi == n) {
+  // source-blocked copy for the remainder pass (appnp_propagate on a full graph,
+  // appnp_step_split on the held rows of a row-partitioned one).  Best-effort: a graph too
+  // large for the copy (block or segment count, device memory) keeps whole-row gathers --
+  // appnp_graph_source_blocks reports whether it was built.
+  if (rc == APPNP_OK && want_sb) {
     const int sb = appnp::graph_build_source_blocks(g, sb_lpe, as_stream(stream));
     if (sb != APPNP_OK && sb != APPNP_ENOTSUP && sb != APPNP_ERANGE && sb != APPNP_ENOMEM)
       rc = sb;
@@ -324,9 +345,17 @@ size_t appnp_workspace_bytes(const appnp_graph* g, int64_t f, int64_t ld, int dt
   if (!g || f < 0 || !valid_dtype(dtype)) return 0;
   (void)ld;  // the workspace uses its own line-aligned leading dimension
   const int64_t rows = g->row_hi - g->row_lo;
-  // two ping-pong buffers (the forward needs one -- two in the split layout, each as large
-  // as a packed buffer -- the adjoint two), 256-B aligned each
-  return (size_t)(2 * rows * line_ld(f, dtype) * elem_size(dtype) + 2048);
+  // two ping-pong buffers (the forward needs one, the adjoint two), 256-B aligned each
+  int64_t need = 2 * rows * line_ld(f, dtype) * elem_size(dtype) + 2048;
+  // the split layout: two buffers [n, fs] + [n, 4 rb_lpe] (a W8 / W16 remainder row is wider
+  // than the packed row's tail), plus the alignment of the base
+  const int64_t r = (g->row_lo == 0 && g->row_hi == g->n) ? remainder_cols(g, f, dtype, true) : 0;
+  if (r > 0) {
+    int64_t main_b = 0, buf_b = 0;
+    split_sizes(g, rows, f - r, &main_b, &buf_b);
+    need = std::max<int64_t>(need, 2 * buf_b + 256);
+  }
+  return (size_t)need;
 }
 
 int appnp_graph_source_blocks(const appnp_graph* g, int64_t* bytes) {
@@ -339,15 +368,27 @@ int appnp_graph_source_blocks(const appnp_graph* g, int64_t* bytes) {
   return APPNP_OK;
 }
 
+int appnp_graph_source_block_layout(const appnp_graph* g, int* width, int64_t* entries,
+                                    int* value_free, int* row_passes, int64_t* launches) {
+  if (!g) return APPNP_EINVAL;
+  const bool built = g->rb_off != nullptr;
+  if (width) *width = built ? 4 * g->rb_lpe : 0;
+  if (entries) *entries = built ? g->rb_total : 0;
+  if (value_free) *value_free = built && g->rb_val == nullptr ? 1 : 0;
+  if (row_passes) *row_passes = built ? g->rb_passes : 0;
+  if (launches) *launches = g->rem_launches.load(std::memory_order_relaxed);
+  return APPNP_OK;
+}
+
 int appnp_propagate_split_point(const appnp_graph* g, int64_t f, int dtype, int64_t* fs) {
   if (!g || !fs || f < 0 || !valid_dtype(dtype)) return APPNP_EINVAL;
-  *fs = split_point(g, f, dtype, dtype == APPNP_F32 ? 4 : 8);
+  *fs = split_point(g, f, dtype, true);
   return APPNP_OK;
 }
 
 int appnp_propagate_remainder_cols(const appnp_graph* g, int64_t f, int dtype, int64_t* r) {
   if (!g || !r || f < 0 || !valid_dtype(dtype)) return APPNP_EINVAL;
-  *r = remainder_cols(g, f, dtype, dtype == APPNP_F32 ? 4 : 8);
+  *r = remainder_cols(g, f, dtype, true);
   return APPNP_OK;
 }
 
@@ -381,13 +422,15 @@ int appnp_propagate(const appnp_graph* g, const void* H, int64_t ld_h, void* Z, 
   StepArgs a = base_args(g, f, alpha);
   a.h = H;
   a.ld_h = ld_h;
-  const int64_t r = K >= 2 ? remainder_cols(g, f, dtype, V) : 0;
+  const int64_t hz_lds[2] = {ld_h, ld_z};
+  const void* hz[2] = {H, Z};
+  const int64_t r = K >= 2 ? remainder_cols(g, f, dtype, vec16(hz_lds, 2, hz, 2)) : 0;
   if (r > 0) {
     // two split buffers [n, fs] + [n, 4 rb_lpe] fp32 in the workspace, each 256-B aligned
     // (fs = 0: narrow rows, all in the remainder pass)
     const int64_t fs = f - r;
-    const int64_t main_b = (n * fs * 4 + 255) / 256 * 256;
-    const int64_t buf_b = (main_b + n * 16 * g->rb_lpe + 255) / 256 * 256;
+    int64_t main_b = 0, buf_b = 0;
+    split_sizes(g, n, fs, &main_b, &buf_b);
     const size_t used = (size_t)(reinterpret_cast<uintptr_t>(ws) -
                                  reinterpret_cast<uintptr_t>(ws_orig));
     if (ws_bytes >= used + 2 * (size_t)buf_b)
@@ -454,13 +497,15 @@ int appnp_propagate_bwd(const appnp_graph* g, const void* dZ, int64_t ld_dz, voi
   rc = dev_err(appnp::launch_scale_rows(dtype, dZ, ld_dz, dH, ld_dh, n, f, alpha, s));
   if (rc) return rc;
   // split rows (self-adjoint A_hat: the source-blocked copy of A_hat is that of A_hat^T)
-  const int64_t r = (self_adjoint && K >= 2) ? remainder_cols(g, f, dtype, V) : 0;
+  const int64_t dd_lds[2] = {ld_dz, ld_dh};
+  const void* dd[2] = {dZ, dH};
+  const int64_t r =
+      (self_adjoint && K >= 2) ? remainder_cols(g, f, dtype, vec16(dd_lds, 2, dd, 2)) : 0;
   const int64_t fs = f - r;
   int64_t main_b = 0, buf_b = 0;
   bool split = r > 0;
   if (split) {
-    main_b = (n * fs * 4 + 255) / 256 * 256;
-    buf_b = (main_b + n * 16 * g->rb_lpe + 255) / 256 * 256;
+    split_sizes(g, n, fs, &main_b, &buf_b);
     const size_t used = (size_t)(reinterpret_cast<uintptr_t>(ws) -
                                  reinterpret_cast<uintptr_t>(ws_orig));
     if (ws_bytes < used + 2 * (size_t)buf_b) split = false;  // too small: whole rows
@@ -587,6 +632,119 @@ int appnp_step(const appnp_graph* g, int part, const void* Zin, int64_t ld_in, c
   }
   const int V = appnp::pick_vec(dtype, f, lds, n_ld, ptrs, 4);
   return dev_err(appnp::launch_step(dtype, epi, V, a, as_stream(stream)));
+}
+
+// ---- the split layout on the held rows of a row-partitioned graph -------------------------
+
+namespace {
+
+// remainder columns of a held-rows split step (appnp_step_split / appnp_split_copy); 0: none
+int64_t rows_split(const appnp_graph* g, int64_t f) {
+  return g ? remainder_cols(g, f, APPNP_F32, true) : 0;
+}
+
+}  // namespace
+
+int appnp_split_layout(const appnp_graph* g, int64_t f, int64_t* fs, int64_t* rem_width) {
+  if (!g || f < 0) return APPNP_EINVAL;
+  const int64_t r = rows_split(g, f);
+  if (fs) *fs = r ? f - r : 0;
+  if (rem_width) *rem_width = r ? 4 * (int64_t)g->rb_lpe : 0;
+  return r ? APPNP_OK : APPNP_ENOTSUP;
+}
+
+int appnp_split_copy(const appnp_graph* g, const float* H, int64_t ld_h, int64_t f, float* main,
+                     float* rem, void* stream) {
+  if (!g || f <= 0) return APPNP_EINVAL;
+  const int64_t r = rows_split(g, f);
+  if (!r) return APPNP_ENOTSUP;
+  const int64_t rows = g->row_hi - g->row_lo, fs = f - r, rw = 4 * (int64_t)g->rb_lpe;
+  if (rows == 0) return APPNP_OK;
+  const int64_t lds[1] = {ld_h};
+  const void* ptrs[3] = {H, main, rem};
+  if (!H || !rem || (fs > 0 && !main) || ld_h < f || !vec16(lds, 1, ptrs, 3)) return APPNP_EINVAL;
+  const float* sc = appnp::remainder_scale(g);
+  return dev_err(appnp::launch_split_copy(H, ld_h, rows, f, fs, rw,
+                                          main ? main + g->row_lo * fs : nullptr,
+                                          rem + g->row_lo * rw, sc ? sc + g->row_lo : nullptr,
+                                          as_stream(stream)));
+}
+
+int appnp_step_split(const appnp_graph* g, int part, const float* zin_main, const float* zin_rem,
+                     const float* H, int64_t ld_h, float* zout_main, float* zout_rem, float* Z,
+                     int64_t ld_z, float* partial, int64_t ld_partial, int64_t f, int k,
+                     float alpha, float p_drop, uint64_t seed, void* stream) {
+  int rc = check_common(g, f, APPNP_F32, 0, alpha, p_drop);
+  if (rc) return rc;
+  if (k < 0 || part < APPNP_PART_ALL || part > APPNP_PART_REMOTE) return APPNP_EINVAL;
+  const int64_t r = rows_split(g, f);
+  if (!r) return APPNP_ENOTSUP;
+  const int64_t rows = g->row_hi - g->row_lo, fs = f - r, rw = 4 * (int64_t)g->rb_lpe;
+  if (rows == 0 || f == 0) return APPNP_OK;
+  if (part != APPNP_PART_ALL && (!g->split || fs == 0)) return APPNP_EINVAL;
+  const bool to_z = Z != nullptr;
+  // inputs: every row of both parts (the remainder only where the pass runs)
+  if (fs > 0 && !zin_main) return APPNP_EINVAL;
+  if (part != APPNP_PART_LOCAL && !zin_rem) return APPNP_EINVAL;
+  if (part != APPNP_PART_LOCAL && (!H || ld_h < f)) return APPNP_EINVAL;
+  if (part != APPNP_PART_LOCAL && !to_z && (!zout_rem || (fs > 0 && !zout_main)))
+    return APPNP_EINVAL;
+  if (to_z && ld_z < f) return APPNP_EINVAL;
+  if (part != APPNP_PART_ALL && (!partial || ld_partial < fs)) return APPNP_EINVAL;
+  const int64_t lds[3] = {part != APPNP_PART_LOCAL ? ld_h : 4, to_z ? ld_z : 4,
+                          part != APPNP_PART_ALL ? ld_partial : 4};
+  const void* ptrs[8] = {zin_main, zin_rem, H, zout_main, zout_rem, Z, partial, nullptr};
+  if (!vec16(lds, 3, ptrs, 7)) return APPNP_EINVAL;
+  const hipStream_t s = as_stream(stream);
+  StepArgs a = base_args(g, f, alpha);
+  set_drop(a, p_drop, seed, k);
+  if (fs > 0) {
+    StepArgs am = a;
+    am.f = (int32_t)fs;
+    am.zin = zin_main;
+    am.ld_in = fs;
+    am.out = to_z ? static_cast<void*>(Z) : static_cast<void*>(zout_main + g->row_lo * fs);
+    am.ld_out = to_z ? ld_z : fs;
+    int epi = appnp::EPI_FWD;
+    if (part == APPNP_PART_ALL) {
+      am.h = H;
+      am.ld_h = ld_h;
+    } else {
+      am.heavy = nullptr;  // the heavy / hub lists describe the full rows, not their halves
+      am.n_heavy = 0;
+      am.hub = nullptr;
+      am.n_hub = 0;
+      if (part == APPNP_PART_LOCAL) {
+        epi = appnp::EPI_PARTIAL;
+        am.nnz = g->nnz_local;
+        am.row_ptr = g->lrow_ptr;
+        am.col = g->lcol;
+        am.val = g->lval;
+        am.out = partial;
+        am.ld_out = ld_partial;
+      } else {
+        epi = appnp::EPI_FINISH;
+        am.nnz = g->nnz_remote;
+        am.row_ptr = g->rrow_ptr;
+        am.col = g->rcol;
+        am.val = g->rval;
+        am.h = H;
+        am.ld_h = ld_h;
+        am.aux = partial;
+        am.ld_aux = ld_partial;
+      }
+    }
+    rc = dev_err(appnp::launch_step(APPNP_F32, epi, 4, am, s));
+    if (rc) return rc;
+  }
+  if (part == APPNP_PART_LOCAL) return APPNP_OK;  // the pass needs every row of zin_rem
+  // the remainder pass over every source block: into the next remainder buffer at the held
+  // rows (a unit graph stores dr o y there), or into Z's last r columns
+  const int nv = (g->rb_lpe == 1 && !to_z) ? 4 : (int)r;
+  g->rem_launches.fetch_add(1, std::memory_order_relaxed);
+  return dev_err(appnp::launch_remainder(g, a, appnp::EPI_FWD, zin_rem, H + fs, ld_h,
+                                         to_z ? Z + fs : zout_rem + g->row_lo * rw,
+                                         to_z ? ld_z : rw, nv, !to_z, s));
 }
 
 // ---- captured plans: the K launches of appnp_propagate replayed as one hipGraph -----------

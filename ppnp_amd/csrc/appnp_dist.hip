@@ -18,6 +18,12 @@
 // The two buffers alternate, and each exchange is waited for before its buffer is written
 // again.  So the only concurrent accesses are the exchange of src, which writes the other
 // ranks' shards, and the local-column step, which reads this rank's shard.
+//
+// Split rows (fp32 F = 32q + r, a graph built with a source-blocked copy of the held rows,
+// appnp_step_split): each iterate is kept as two full-height parts, main [P S, 32q] (whole
+// cache lines per gathered row) and remainder [P S, width of the copy]; both are exchanged
+// (two all-gather calls per exchange), the main part runs the SpMM kernel (local / remote with
+// overlap) and the remainder part the persistent L2-blocked pass once the exchange has landed.
 #include <dlfcn.h>
 
 #include <algorithm>
@@ -58,17 +64,91 @@ struct WsLayout {
   size_t buf_bytes = 0;    // one full-height iterate
   size_t partial_off = 0;  // fp32 partial (overlap)
   size_t total = 0;
+  // split rows: main [P S, fs] and remainder [P S, rw] parts of each iterate
+  int64_t fs = 0, rw = 0;
+  size_t main_bytes = 0, part_bytes = 0;  // one main part; one iterate (main + remainder)
+  size_t split_total = 0;
 };
 
 WsLayout ws_layout(const appnp_dist* d, int64_t f, int dtype) {
   WsLayout w;
   const int64_t es = dtype == APPNP_F32 ? 4 : 2;
+  const size_t rows_pad = (size_t)(d->shard * d->nranks);
   w.ld = appnp::line_ld(f, dtype);
-  w.buf_bytes = align_up((size_t)(d->shard * d->nranks) * (size_t)(w.ld * es));
+  w.buf_bytes = align_up(rows_pad * (size_t)(w.ld * es));
   w.partial_off = 2 * w.buf_bytes;
   const size_t partial = d->overlap ? align_up((size_t)d->shard * (size_t)w.ld * 4) : 0;
   w.total = w.partial_off + partial;
+  if (dtype == APPNP_F32 && appnp_split_layout(d->g, f, &w.fs, &w.rw) == APPNP_OK) {
+    w.main_bytes = align_up(rows_pad * (size_t)w.fs * 4);
+    w.part_bytes = w.main_bytes + align_up(rows_pad * (size_t)w.rw * 4);
+    w.split_total = 2 * w.part_bytes + (d->overlap ? align_up((size_t)d->shard * w.fs * 4) : 0);
+  }
   return w;
+}
+
+bool aligned16(const void* p, int64_t ld) {
+  return ld % 4 == 0 && (reinterpret_cast<uintptr_t>(p) % 16) == 0;
+}
+
+// The loop of appnp_dist_propagate on the split layout (see the file comment).
+int propagate_split_rows(appnp_dist* d, const WsLayout& w, const float* H, int64_t ld_h, float* Z,
+                         int64_t ld_z, int64_t f, int K, float alpha, float p_drop,
+                         uint64_t seed, char* base, hipStream_t s) {
+  float* mainb[2] = {reinterpret_cast<float*>(base),
+                     reinterpret_cast<float*>(base + w.part_bytes)};
+  float* remb[2] = {reinterpret_cast<float*>(base + w.main_bytes),
+                    reinterpret_cast<float*>(base + w.part_bytes + w.main_bytes)};
+  float* partial = d->overlap ? reinterpret_cast<float*>(base + 2 * w.part_bytes) : nullptr;
+  const size_t main_shard = (size_t)d->shard * (size_t)w.fs * 4;
+  const size_t rem_shard = (size_t)d->shard * (size_t)w.rw * 4;
+  auto exchange = [&](int b, hipStream_t xs) {
+    int rc = APPNP_OK;
+    if (w.fs > 0) rc = d->allgather(mainb[b], main_shard, d->rank, d->nranks, xs, d->ctx);
+    if (rc == APPNP_OK) rc = d->allgather(remb[b], rem_shard, d->rank, d->nranks, xs, d->ctx);
+    return rc;
+  };
+  int rc = appnp_split_copy(d->g, H, ld_h, f, w.fs ? mainb[0] : nullptr, remb[0], s);
+  if (rc == APPNP_OK && d->nranks > 1) rc = exchange(0, s);
+  bool pending = false;
+  for (int k = 0; k < K && rc == APPNP_OK; ++k) {
+    const bool last = k == K - 1;
+    const int cur = k & 1, nxt = cur ^ 1;
+    float* zm_out = last ? nullptr : mainb[nxt];
+    float* zr_out = last ? nullptr : remb[nxt];
+    float* zout = last ? Z : nullptr;
+    if (d->overlap && w.fs > 0) {
+      rc = appnp_step_split(d->g, APPNP_PART_LOCAL, mainb[cur], remb[cur], H, ld_h, zm_out, zr_out,
+                            zout, ld_z, partial, w.fs, f, k, alpha, p_drop, seed, s);
+      if (rc == APPNP_OK && pending) {
+        rc = dev_err(hipStreamWaitEvent(s, d->exchanged, 0));
+        pending = false;
+      }
+      if (rc == APPNP_OK)
+        rc = appnp_step_split(d->g, APPNP_PART_REMOTE, mainb[cur], remb[cur], H, ld_h, zm_out,
+                              zr_out, zout, ld_z, partial, w.fs, f, k, alpha, p_drop, seed, s);
+    } else {
+      if (pending) {
+        rc = dev_err(hipStreamWaitEvent(s, d->exchanged, 0));
+        pending = false;
+      }
+      if (rc == APPNP_OK)
+        rc = appnp_step_split(d->g, APPNP_PART_ALL, mainb[cur], remb[cur], H, ld_h, zm_out,
+                              zr_out, zout, ld_z, nullptr, 0, f, k, alpha, p_drop, seed, s);
+    }
+    if (rc != APPNP_OK || last || d->nranks == 1) continue;
+    if (d->overlap) {
+      rc = dev_err(hipEventRecord(d->produced, s));
+      if (rc == APPNP_OK) rc = dev_err(hipStreamWaitEvent(d->xs, d->produced, 0));
+      if (rc == APPNP_OK) rc = exchange(nxt, d->xs);
+      if (rc == APPNP_OK) rc = dev_err(hipEventRecord(d->exchanged, d->xs));
+      pending = rc == APPNP_OK;
+    } else {
+      rc = exchange(nxt, s);
+    }
+  }
+  if (pending) (void)hipStreamWaitEvent(s, d->exchanged, 0);
+  return rc;
 }
 
 // rows x (f elements) between two row-major matrices with leading dimensions in elements
@@ -148,7 +228,8 @@ const appnp_graph* appnp_dist_graph(const appnp_dist* d) { return d ? d->g : nul
 
 size_t appnp_dist_workspace_bytes(const appnp_dist* d, int64_t f, int dtype) {
   if (!d || f <= 0 || (dtype != APPNP_F32 && dtype != APPNP_BF16)) return 0;
-  return ws_layout(d, f, dtype).total;
+  const WsLayout w = ws_layout(d, f, dtype);
+  return std::max(w.total, w.split_total);
 }
 
 int appnp_dist_propagate(appnp_dist* d, const void* H, int64_t ld_h, void* Z, int64_t ld_z,
@@ -165,6 +246,13 @@ int appnp_dist_propagate(appnp_dist* d, const void* H, int64_t ld_h, void* Z, in
   hipStream_t s = as_stream(stream);
   if (K == 0) return dev_err(copy_rows(Z, ld_z, H, ld_h, rows, f, es, s));
   const WsLayout w = ws_layout(d, f, dtype);
+  // split rows when the held rows' copy allows it and H / Z allow 16-B vectors (K >= 2: one
+  // iteration gains nothing from the split layout)
+  if (w.split_total && K >= 2 && (rows == 0 || (aligned16(H, ld_h) && aligned16(Z, ld_z)))) {
+    if (!ws || ws_bytes < w.split_total) return APPNP_EINVAL;
+    return propagate_split_rows(d, w, static_cast<const float*>(H), ld_h, static_cast<float*>(Z),
+                                ld_z, f, K, alpha, p_drop, seed, static_cast<char*>(ws), s);
+  }
   if (!ws || ws_bytes < w.total) return APPNP_EINVAL;
   char* base = static_cast<char*>(ws);
   char* buf[2] = {base, base + w.buf_bytes};

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+
 #include "appnp_device.h"
 #include "../../include/ppnp_amd.h"
 
@@ -58,6 +60,9 @@ struct appnp_graph {
   int32_t rb_passes = 0;
   int32_t rb_lpe = 0;           // lanes per entry of the pass: remainder rows of 4 rb_lpe columns
   double near_frac = 0.0;       // off-diagonal entries within kNearRows of their row / nnz
+  // remainder-pass launches enqueued on this graph (appnp_graph_source_block_layout): the path
+  // witness the tests read
+  mutable std::atomic<int64_t> rem_launches{0};
 };
 
 struct appnp_csr;

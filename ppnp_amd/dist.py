@@ -329,7 +329,7 @@ class PartitionedAPPNP:
     """K-iteration APPNP over a Layout of ranks.  Build with :meth:`create`."""
 
     def __init__(self, layout, rank, n, f, K, alpha, graph, H_slab, f_lo, f_hi, bufs, shard,
-                 lo, hi, comm, step_fn, overlap, partial, p_drop=0.0, seed=0):
+                 lo, hi, comm, step_fn, overlap, partial, p_drop=0.0, seed=0, split=None):
         self.layout, self.rank = layout, rank
         self.n, self.f, self.K, self.alpha = n, f, K, alpha
         self.graph = graph
@@ -340,6 +340,10 @@ class PartitionedAPPNP:
         self.comm, self.step_fn = comm, step_fn
         self.overlap, self.partial = overlap, partial
         self.p_drop, self.seed = p_drop, seed
+        # split rows on the held rows (row groups, appnp_step_split): (fs, rem width), the two
+        # full-height parts of both iterates and the held rows' output
+        self.split = split
+        self.smain = self.srem = self.zout = None
         self.out = None
 
     # -- construction ---------------------------------------------------------------------
@@ -379,29 +383,51 @@ class PartitionedAPPNP:
             # layout) on a slab whose rows split (graph.remainder_width: fp32, width 32q + r
             # with r <= 16, or a narrow slab of <= 16 columns, e.g. 12-13 of F = 100 on 8
             # ranks); appnp_step gathers whole rows
+            # a column-layout rank runs appnp_propagate on its slab, a row-group rank
+            # appnp_step_split on its held rows: both split like one GPU when the slab's rows do
+            # (graph.remainder_width: fp32, width 32q + r with r <= 8, or a narrow slab of <= 16
+            # columns), from the source-blocked copy of the rows the rank holds
             graph = Graph.from_csr(indptr, indices, data, n, mode=mode, device=device,
-                                   row_lo=lo, row_hi=hi, split_local=overlap,
-                                   features=width if layout.rows == 1 else None,
+                                   row_lo=lo, row_hi=hi, split_local=overlap, features=width,
                                    dtype=H.dtype)
         else:
             graph = graph_fn(lo, hi, overlap)
         rows_pad = shard * layout.rows
         H_slab = torch.zeros(max(hi - lo, 0), ld, dtype=H.dtype, device=device)
         H_slab[:, :width] = H[lo:hi, f_lo:f_hi].to(device)
-        bufs = [torch.zeros(rows_pad, ld, dtype=H.dtype, device=device) for _ in range(2)]
-        partial = (torch.zeros(max(hi - lo, 0), ld, dtype=torch.float32, device=device)
-                   if overlap else None)
+        split = None
+        if (layout.rows > 1 and step_fn is None and K >= 2 and H.dtype == torch.float32
+                and ld % 4 == 0 and hasattr(graph, "split_layout")):
+            split = graph.split_layout(width)
+        if split is None:
+            bufs = [torch.zeros(rows_pad, ld, dtype=H.dtype, device=device) for _ in range(2)]
+            partial = (torch.zeros(max(hi - lo, 0), ld, dtype=torch.float32, device=device)
+                       if overlap else None)
+        else:
+            bufs = []
+            fs = split[0]
+            partial = (torch.zeros(max(hi - lo, 0), max(fs, 4), dtype=torch.float32,
+                                   device=device) if overlap and fs > 0 else None)
         if comm is None:
             if exchange not in ("multipath", "group"):
                 raise ValueError(f"unknown exchange {exchange!r}")
-            widths = [col_range(f, layout.cols, c)[1] - col_range(f, layout.cols, c)[0]
-                      for c in range(layout.cols)]
+            # split parts travel whole (their padding is zero on every rank)
+            widths = None if split else [
+                col_range(f, layout.cols, c)[1] - col_range(f, layout.cols, c)[0]
+                for c in range(layout.cols)]
             comm = (MultipathComm(layout, rank, widths)
                     if exchange == "multipath" and layout.rows > 1 and layout.cols > 1
                     else _TorchComm(layout, rank))
         step_fn = step_fn or _hip_step
         obj = cls(layout, rank, n, f, K, alpha, graph, H_slab, f_lo, f_hi, bufs, shard, lo, hi,
-                  comm, step_fn, overlap, partial, p_drop, seed)
+                  comm, step_fn, overlap, partial, p_drop, seed, split)
+        if split is not None:
+            fs, rw = split
+            obj.smain = ([torch.zeros(rows_pad, fs, dtype=torch.float32, device=device)
+                          for _ in range(2)] if fs > 0 else [None, None])
+            obj.srem = [torch.zeros(rows_pad, rw, dtype=torch.float32, device=device)
+                        for _ in range(2)]
+            obj.zout = torch.zeros(max(hi - lo, 0), ld, dtype=torch.float32, device=device)
         obj.exchange = getattr(comm, "name", "group")
         return obj
 
@@ -410,10 +436,71 @@ class PartitionedAPPNP:
         return self.graph.nnz_hat
 
     @property
+    def remainder_cols(self) -> int:
+        """Columns of this rank's slab that run the L2-blocked remainder pass per iteration (0:
+        whole rows): a column-layout rank runs appnp_propagate on its slab, which splits like a
+        single GPU (appnp_propagate_remainder_cols); a row-group rank runs appnp_step_split
+        when its rows split."""
+        if self.split is not None:
+            return self.width - self.split[0]
+        if self.layout.rows == 1 and self.step_fn is _hip_step and self.K >= 2:
+            return self.graph.remainder_cols(self.width, self.H.dtype)
+        return 0
+
+    @property
     def width(self) -> int:
         return self.f_hi - self.f_lo
 
     # -- the K loop -----------------------------------------------------------------------
+    def _exchange_split(self, b: int, async_op: bool):
+        """All-gather both parts of split iterate ``b``; the handles to wait for."""
+        works = []
+        for t in (self.smain[b], self.srem[b]):
+            if t is not None:
+                w = self.comm.all_gather_rows(t, self.shard, async_op=async_op)
+                if w is not None:
+                    works.append(w)
+        return works
+
+    def _run_split(self):
+        """The row-group loop on the split layout (appnp_step_split): the main columns gather
+        whole lines (local / remote parts with overlap), the remainder columns run the
+        L2-blocked pass once the exchange of the iterate has landed."""
+        from .ops import split_copy, step_split
+
+        K, w, g = self.K, self.width, self.graph
+        fs, _ = self.split
+        H = self.H[:, :w]
+        split_copy(g, H, self.smain[0], self.srem[0])
+        works = self._exchange_split(0, async_op=False)
+        kw = dict(p_drop=self.p_drop, seed=self.seed)
+        for k in range(K):
+            cur, nxt = k & 1, (k & 1) ^ 1
+            last = k == K - 1
+            outs = dict(out_main=None if last else self.smain[nxt],
+                        out_rem=None if last else self.srem[nxt],
+                        Z=self.zout[:, :w] if last else None)
+            zin = (self.smain[cur], self.srem[cur])
+            if self.overlap and fs > 0:
+                step_split(g, _lib.PART_LOCAL, zin[0], zin[1], None, w, k, self.alpha,
+                           partial=self.partial[:, :fs], **kw)
+                for wk in works:
+                    wk.wait()
+                works = []
+                step_split(g, _lib.PART_REMOTE, zin[0], zin[1], H, w, k, self.alpha,
+                           partial=self.partial[:, :fs], **outs, **kw)
+            else:
+                for wk in works:
+                    wk.wait()
+                works = []
+                step_split(g, _lib.PART_ALL, zin[0], zin[1], H, w, k, self.alpha, **outs, **kw)
+            if not last:
+                works = self._exchange_split(nxt, async_op=self.overlap)
+        for wk in works:
+            wk.wait()
+        self.out = self.zout[:, :w]
+        return self.out
+
     def run(self):
         """Z_K for this rank's rows x feature slab; returns a [hi-lo, width] view."""
         K, R = self.K, self.layout.rows
@@ -422,6 +509,8 @@ class PartitionedAPPNP:
         if K == 0:
             self.out = self.H[:, :w]
             return self.out
+        if self.split is not None:
+            return self._run_split()
         if R == 1 and self.step_fn is _hip_step:
             # column layout: this rank holds every row of its slab, so the K iterations are one
             # appnp_propagate call (no per-iteration host work between the launches)
@@ -496,8 +585,13 @@ class NativeRowAPPNP:
     and runs it with the same arguments."""
 
     def __init__(self, indptr, indices, n, device, overlap=True, mode="sym", data=None,
-                 exchange=None, rank=None, world=None):
+                 exchange=None, rank=None, world=None, features=None, dtype=torch.float32):
+        """features: the F the engine will propagate; when fp32 rows of that width split
+        (graph.remainder_width), the held rows get a source-blocked copy and the engine runs the
+        split layout (appnp_step_split)."""
         import ctypes as C
+
+        from .graph import remainder_width
 
         lib = _lib.load()
         self.device = torch.device(device)
@@ -524,10 +618,12 @@ class NativeRowAPPNP:
         val = None if data is None else data.to(self.device, torch.float32).contiguous()
         h = C.c_void_p()
         stream = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        w = remainder_width(n, int(features), dtype) if features else 0
+        sb = {0: 0, 4: _lib.GRAPH_SOURCE_BLOCKS, 8: _lib.GRAPH_SB_W8, 16: _lib.GRAPH_SB_W16}[w]
         _lib.check("appnp_dist_create", lib.appnp_dist_create(
             C.c_void_p(ip.data_ptr()), C.c_void_p(ix.data_ptr()) if ix.numel() else None,
             C.c_void_p(val.data_ptr()) if val is not None and val.numel() else None, n,
-            ix.numel(), _lib.NORM[mode], self.rank, self.world, int(bool(overlap)), fn, ctx,
+            ix.numel(), _lib.NORM[mode] | sb, self.rank, self.world, int(bool(overlap)), fn, ctx,
             stream, C.byref(h)))
         self._h = h
         lo, hi, shard = C.c_int64(), C.c_int64(), C.c_int64()
@@ -589,6 +685,7 @@ class _DistGraphInfo:
     def __init__(self, handle):
         import ctypes as C
 
+        self._h = handle
         n, lo, hi, nnz = C.c_int64(), C.c_int64(), C.c_int64(), C.c_int64()
         mode, sym = C.c_int(), C.c_int()
         _lib.check("appnp_graph_info", _lib.load().appnp_graph_info(
@@ -597,6 +694,16 @@ class _DistGraphInfo:
         self.n, self.row_lo, self.row_hi = n.value, lo.value, hi.value
         self.rows = hi.value - lo.value
         self.nnz_hat = nnz.value
+
+    def source_block_layout(self):
+        from .graph import source_block_layout_of
+
+        return source_block_layout_of(self._h)
+
+    def split_layout(self, f: int):
+        from .graph import split_layout_of
+
+        return split_layout_of(self._h, f)
 
 
 class NativeRowRunner:
@@ -609,7 +716,7 @@ class NativeRowRunner:
     def __init__(self, indptr, indices, n, H, K, alpha, device, overlap=True, mode="sym",
                  data=None, p_drop=0.0, seed=0):
         self.engine = NativeRowAPPNP(indptr, indices, n, device, overlap=overlap, mode=mode,
-                                     data=data)
+                                     data=data, features=int(H.shape[1]), dtype=H.dtype)
         self.layout = Layout(self.engine.world, 1)
         self.rank = self.engine.rank
         self.overlap = bool(overlap and self.engine.world > 1)
@@ -621,6 +728,10 @@ class NativeRowRunner:
         import ctypes as C
 
         self.graph = _DistGraphInfo(C.c_void_p(_lib.load().appnp_dist_graph(self.engine._h)))
+        # the split the engine takes (appnp_dist_propagate: fp32, K >= 2, 16-B aligned H / Z)
+        sp = self.graph.split_layout(self.width) if H.dtype == torch.float32 else None
+        aligned = self.H.stride(0) % 4 == 0 and self.H.data_ptr() % 16 == 0
+        self.remainder_cols = (self.width - sp[0]) if sp and K >= 2 and aligned else 0
 
     @property
     def width(self) -> int:
@@ -674,11 +785,15 @@ def fits(layout: Layout, n: int, f: int, nnz_hat: int, elem_bytes: int = 4,
 
 def candidate_layouts(world: int, f: int, n: int = 0, nnz_hat: int = 0, elem_bytes: int = 4,
                       mem_bytes: int | None = None):
-    """(layout, overlap, exchange) variants ``bench.py --layout auto`` times after warm-up,
-    keeping the fastest (max over ranks).  The column partition needs no exchange; from 8 ranks
-    on, 2 row groups halve each rank's gathers for an exchange of half a slab per iteration,
-    which only an xGMI measurement can price.  Candidates that do not
-    fit (``fits``) are dropped; if none does, the row-heaviest layout that fits is used."""
+    """(layout, overlap, exchange) variants ``bench.py --layout auto`` measures, the fastest of
+    which it reports (max over ranks).  The first is ``choose_layout``'s: the column partition,
+    which needs no exchange, whenever it fits.  From 4 ranks on, the two 2-D layouts with 2 row
+    groups or 2 column groups -- 2 x (P/2) (half of each rank's gathers for half a slab of
+    exchange) and (P/2) x 2 (a quarter of the rows on 8 ranks, two-line gathers) -- each with the
+    relayed and the group exchange, which only an xGMI measurement can price (DESIGN.md section
+    5).  Then the north_star's pure row partition (overlapped all-gather, and the library's own
+    loop).  Candidates that do not fit (``fits``) are dropped; if none does, the row-heaviest
+    layout that fits is used."""
     first = choose_layout(world, n, f, nnz_hat, elem_bytes, mem_bytes)
     row = Layout(world, 1)
     # the north_star's design -- a pure row partition, all-gather overlapped with the local
@@ -690,10 +805,14 @@ def candidate_layouts(world: int, f: int, n: int = 0, nnz_hat: int = 0, elem_byt
                  [(first, True, "group")])
         return cands + [c for c in row_cand if c[0] != first]
     cands = [(first, False, "group")]
-    if world >= 8 and world % 2 == 0 and f >= world // 2:
-        two = Layout(2, world // 2)
-        if fits(two, n, f, nnz_hat, elem_bytes, True, mem_bytes):
-            cands += [(two, True, "multipath"), (two, True, "group")]
+    if world >= 4 and world % 2 == 0:
+        seen = {first}
+        for lay in (Layout(2, world // 2), Layout(world // 2, 2)):
+            if lay in seen or lay.rows == world or f < lay.cols:
+                continue
+            seen.add(lay)
+            if fits(lay, n, f, nnz_hat, elem_bytes, True, mem_bytes):
+                cands += [(lay, True, "multipath"), (lay, True, "group")]
     return cands + [c for c in row_cand if c[0] != first]
 
 

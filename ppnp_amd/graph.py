@@ -48,6 +48,30 @@ def splits_rows(n: int, features: int, dtype=torch.float32) -> bool:
     return remainder_width(n, features, dtype) > 0
 
 
+def source_block_layout_of(handle):
+    """``Graph.source_block_layout`` for any graph handle (also an appnp_dist engine's)."""
+    w, vf, rp = C.c_int(), C.c_int(), C.c_int()
+    ent, launches = C.c_int64(), C.c_int64()
+    _lib.check("appnp_graph_source_block_layout",
+               _lib.load().appnp_graph_source_block_layout(
+                   handle, C.byref(w), C.byref(ent), C.byref(vf), C.byref(rp),
+                   C.byref(launches)))
+    if w.value == 0:
+        return None
+    return {"width": w.value, "entries": ent.value, "value_free": bool(vf.value),
+            "row_passes": rp.value, "launches": launches.value}
+
+
+def split_layout_of(handle, f: int):
+    """``Graph.split_layout`` for any graph handle."""
+    fs, rw = C.c_int64(), C.c_int64()
+    rc = _lib.load().appnp_split_layout(handle, int(f), C.byref(fs), C.byref(rw))
+    if rc == _lib.APPNP_ENOTSUP:
+        return None
+    _lib.check("appnp_split_layout", rc)
+    return fs.value, rw.value
+
+
 class Graph:
     """A_hat = calc_A_hat(adj, mode) held on one GPU (all rows, or rows [row_lo, row_hi)).
 
@@ -118,11 +142,12 @@ class Graph:
         nnz = int(ix.numel())
         row_hi = n if row_hi is None else int(row_hi)
         width = 4
-        if features is not None and int(row_lo) == 0 and row_hi == n:
+        if features is not None:
             width = remainder_width(n, int(features), dtype) or 4
         if source_blocks is None:
-            source_blocks = (features is not None and int(row_lo) == 0 and row_hi == n
-                             and splits_rows(n, int(features), dtype))
+            # full graphs (appnp_propagate) and the held rows of a row partition
+            # (appnp_step_split) alike
+            source_blocks = features is not None and splits_rows(n, int(features), dtype)
         sb_flag = {4: _lib.GRAPH_SOURCE_BLOCKS, 8: _lib.GRAPH_SB_W8, 16: _lib.GRAPH_SB_W16}[width]
         flags = ((_lib.GRAPH_TRANSPOSE if transpose else 0)
                  | (sb_flag if source_blocks else 0))
@@ -185,6 +210,17 @@ class Graph:
         _lib.check("appnp_graph_source_blocks",
                    _lib.load().appnp_graph_source_blocks(self._h, C.byref(b)))
         return b.value
+
+    def source_block_layout(self):
+        """The source-blocked copy as built (appnp_graph_source_block_layout): dict(width=4/8/16
+        remainder columns per row, entries incl. padding, value_free, row_passes, launches =
+        remainder-pass launches enqueued on this graph so far), or None when it was not built."""
+        return source_block_layout_of(self._h)
+
+    def split_layout(self, f: int):
+        """(fs, rem_width) of the split layout appnp_step_split uses on the held rows for F = f
+        columns (appnp_split_layout), or None when f does not split on this graph."""
+        return split_layout_of(self._h, f)
 
     def csr(self):
         """(row_ptr int32, col int32, val fp32, dinv fp64) as new device tensors."""

@@ -130,9 +130,12 @@ _propagate_op.register_autograd(_propagate_grad, setup_context=_propagate_setup)
 
 def propagate(graph: Graph, H: torch.Tensor, K: int = 10, alpha: float = 0.1,
               p_drop: float = 0.0, seed: int = 0) -> torch.Tensor:
-    """Differentiable APPNP propagation Z_K(H) on the GPU (the ``ppnp_amd::propagate`` op)."""
+    """Differentiable APPNP propagation Z_K(H) on the GPU (the ``ppnp_amd::propagate`` op).
+    The seed is taken mod 2^64 like everywhere else (propagate_forward, the oracle); it crosses
+    the op's int64 schema reinterpreted as signed, and propagate_forward maps it back."""
+    s = int(seed) & (2**64 - 1)
     return torch.ops.ppnp_amd.propagate(H, graph.key, int(K), float(alpha), float(p_drop),
-                                        int(seed) & (2**63 - 1))
+                                        s - 2**64 if s >= 2**63 else s)
 
 
 def step(graph: Graph, Zin: torch.Tensor, H: torch.Tensor, out: torch.Tensor, k: int,
@@ -151,6 +154,34 @@ def step(graph: Graph, Zin: torch.Tensor, H: torch.Tensor, out: torch.Tensor, k:
                             float(p_drop), int(seed) & (2**64 - 1), _stream(graph.device))
     _lib.check("appnp_step", rc)
     return out
+
+
+def split_copy(graph: Graph, H: torch.Tensor, main: torch.Tensor | None,
+               rem: torch.Tensor) -> None:
+    """Z_0 of the split layout on the held rows (``appnp_split_copy``): H [held rows, F] into
+    rows [row_lo, row_hi) of the full-height parts main [*, fs] and rem [*, rem_width]."""
+    with torch.cuda.device(graph.device):
+        rc = _lib.load().appnp_split_copy(graph.handle, _vp(H), _ld(H), int(H.shape[1]),
+                                          _vp(main), _vp(rem), _stream(graph.device))
+    _lib.check("appnp_split_copy", rc)
+
+
+def step_split(graph: Graph, part: int, zin_main: torch.Tensor | None, zin_rem: torch.Tensor,
+               H: torch.Tensor | None, f: int, k: int, alpha: float,
+               out_main: torch.Tensor | None = None, out_rem: torch.Tensor | None = None,
+               Z: torch.Tensor | None = None, partial: torch.Tensor | None = None,
+               p_drop: float = 0.0, seed: int = 0) -> None:
+    """One iteration of the held rows on the split layout (``appnp_step_split``): from every row
+    of zin_main / zin_rem into rows [row_lo, row_hi) of out_main / out_rem, or into Z (the held
+    rows, all F columns) on the last iteration."""
+    with torch.cuda.device(graph.device):
+        rc = _lib.load().appnp_step_split(
+            graph.handle, int(part), _vp(zin_main), _vp(zin_rem), _vp(H),
+            _ld(H) if H is not None else 0, _vp(out_main), _vp(out_rem), _vp(Z),
+            _ld(Z) if Z is not None else 0, _vp(partial),
+            _ld(partial) if partial is not None else 0, int(f), int(k), float(alpha),
+            float(p_drop), int(seed) & (2**64 - 1), _stream(graph.device))
+    _lib.check("appnp_step_split", rc)
 
 
 class PropagatePlan:

@@ -6,12 +6,18 @@ configs run on uniform random stand-ins with the published node / edge counts:
 m (src, dst) pairs uniform in [0, N), A = A + A^T, data := 1, no self loops, duplicates
 merged -- the reference's ``standardize`` semantics (sparsegraph.py:191-222) without LCC.
 
-This is input synthesis (like torch.randn for H), generated directly on the GPU with torch
-so a 62M-edge graph takes well under a second; it is not part of the measured path.
+The graphs are drawn on the HOST with numpy ``default_rng(seed)`` -- the recipe of SURVEY.md
+section 8(d) and BASELINE.md, so ``uniform_graph`` yields exactly ``oracle.synth_graph``'s
+instance (tests/test_synth.py) -- and H with a CPU ``torch.Generator().manual_seed(seed)``.
+Sorting and de-duplicating on the host (numpy's vectorised sort: ~10 s for products-synth's
+124 M keys) also keeps generation independent of how processes share a GPU: the round-2 device
+generator (torch.unique on the GPU) stalled for minutes when 8 ranks time-sliced one device.
+This is input synthesis, not part of the measured path.
 """
 
 from __future__ import annotations
 
+import numpy as np
 import torch
 
 CONFIGS = {
@@ -47,90 +53,78 @@ for _name in REAL:
     DESCRIPTIONS[_name] = "the reference's dataset (standardized LCC adjacency)"
 
 
-def uniform_graph_device(n: int, m: int, seed: int, device="cuda"):
-    """CSR (indptr int32 [n+1], indices int32 [nnz]) of the symmetrised uniform graph, on
-    ``device``; columns sorted within each row, no duplicates, no self loops."""
-    g = torch.Generator(device=device).manual_seed(seed)
-    src = torch.randint(0, n, (m,), device=device, generator=g, dtype=torch.int64)
-    dst = torch.randint(0, n, (m,), device=device, generator=g, dtype=torch.int64)
+def _csr_from_pairs(src, dst, n: int, device):
+    """Symmetrised, de-duplicated, self-loop-free int32 CSR of the (src, dst) pairs: the
+    pattern of A + A^T with data := 1, setdiag(0), eliminate_zeros (the reference's
+    ``standardize`` semantics without LCC, sparsegraph.py:191-222), columns sorted in each row.
+    Returned as torch tensors on ``device``."""
+    src = np.asarray(src, dtype=np.int64)
+    dst = np.asarray(dst, dtype=np.int64)
     keep = src != dst
     src, dst = src[keep], dst[keep]
-    key = torch.cat([src * n + dst, dst * n + src])
+    key = np.concatenate([src * n + dst, dst * n + src])
     del src, dst, keep
-    key = torch.unique(key, sorted=True)
-    row = torch.div(key, n, rounding_mode="floor")
-    col = (key - row * n).to(torch.int32)
+    key.sort()  # vectorised (x86-simd-sort) quicksort: ~3 s for 124 M int64 keys
+    if key.size:
+        first = np.empty(key.size, dtype=bool)
+        first[0] = True
+        np.not_equal(key[1:], key[:-1], out=first[1:])
+        key = key[first]
+        del first
+    row = key // n
+    col = (key - row * n).astype(np.int32)
     del key
-    counts = torch.bincount(row, minlength=n)
-    indptr = torch.zeros(n + 1, dtype=torch.int64, device=device)
-    indptr[1:] = torch.cumsum(counts, 0)
-    return indptr.to(torch.int32), col
+    indptr = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(np.bincount(row, minlength=n), out=indptr[1:])
+    del row
+    return (torch.from_numpy(indptr.astype(np.int32)).to(device),
+            torch.from_numpy(col).to(device))
 
 
-def chung_lu_graph_device(n: int, m: int, seed: int, exponent: float = 3.2,
-                          device="cuda"):
+def uniform_graph(n: int, m: int, seed: int, device="cuda"):
+    """CSR (indptr int32 [n+1], indices int32 [nnz]) of SURVEY.md 8(d)'s uniform graph: m pairs
+    (src, dst) from ``numpy.random.default_rng(seed)`` (src first, then dst), symmetrised, no
+    self loops, duplicates merged.  Identical to ``oracle.synth_graph(n, m, seed)``."""
+    rng = np.random.default_rng(seed)
+    src = rng.integers(0, n, size=m, dtype=np.int64)
+    dst = rng.integers(0, n, size=m, dtype=np.int64)
+    return _csr_from_pairs(src, dst, n, device)
+
+
+def chung_lu_graph(n: int, m: int, seed: int, exponent: float = 3.2, device="cuda"):
     """Power-law graph (Chung-Lu): endpoints drawn with probability proportional to
-    w_i = (i + 1)^(-1/(exponent-1)) (inverse-CDF sampling), then the same symmetrise /
-    de-duplicate / no-self-loop steps as ``uniform_graph_device``.  Exponent 3.2 gives a
-    largest degree of ~20k at products scale (the real ogbn-products: ~17k, mean ~50)."""
-    g = torch.Generator(device=device).manual_seed(seed)
-    w = torch.arange(1, n + 1, device=device, dtype=torch.float64).pow(-1.0 / (exponent - 1.0))
-    cdf = torch.cumsum(w, 0)
-    cdf /= cdf[-1].clone()
-    u = torch.rand(2, m, device=device, generator=g, dtype=torch.float64)
-    ends = torch.searchsorted(cdf, u).clamp_(max=n - 1)
-    # scatter node ids so hubs are not all at low indices
-    perm = torch.randperm(n, device=device, generator=g)
-    src, dst = perm[ends[0]], perm[ends[1]]
-    del ends, u, cdf, w
-    keep = src != dst
-    src, dst = src[keep], dst[keep]
-    key = torch.cat([src * n + dst, dst * n + src])
-    del src, dst, keep
-    key = torch.unique(key, sorted=True)
-    row = torch.div(key, n, rounding_mode="floor")
-    col = (key - row * n).to(torch.int32)
-    del key
-    counts = torch.bincount(row, minlength=n)
-    indptr = torch.zeros(n + 1, dtype=torch.int64, device=device)
-    indptr[1:] = torch.cumsum(counts, 0)
-    return indptr.to(torch.int32), col
+    w_i = (i + 1)^(-1/(exponent-1)) (inverse-CDF sampling), node ids permuted so hubs are not
+    all at low indices, then the same symmetrise / de-duplicate / no-self-loop steps as
+    ``uniform_graph``.  Exponent 3.2 gives a largest degree of ~20k at products scale (the real
+    ogbn-products: ~17k, mean ~50)."""
+    rng = np.random.default_rng(seed)
+    w = np.arange(1, n + 1, dtype=np.float64) ** (-1.0 / (exponent - 1.0))
+    cdf = np.cumsum(w)
+    cdf /= cdf[-1]
+    ends = np.minimum(np.searchsorted(cdf, rng.random((2, m))), n - 1)
+    perm = rng.permutation(n)
+    return _csr_from_pairs(perm[ends[0]], perm[ends[1]], n, device)
 
 
-def community_graph_device(n: int, m: int, seed: int, block: int = 4096, p_in: float = 0.9,
-                           device="cuda"):
+def community_graph(n: int, m: int, seed: int, block: int = 4096, p_in: float = 0.9,
+                    device="cuda"):
     """Graph with gather locality: the source of each of the m pairs is uniform; with
     probability p_in its destination is uniform inside the source's community (``block``
     consecutive node ids), otherwise uniform over all nodes.  Then the same symmetrise /
-    de-duplicate / no-self-loop steps as ``uniform_graph_device``.  A community's rows of an
+    de-duplicate / no-self-loop steps as ``uniform_graph``.  A community's rows of an
     F = 100 fp32 Z are 1.6 MB, so the rows a wave front gathers stay in L2."""
-    g = torch.Generator(device=device).manual_seed(seed)
-    src = torch.randint(0, n, (m,), device=device, generator=g, dtype=torch.int64)
-    far = torch.randint(0, n, (m,), device=device, generator=g, dtype=torch.int64)
-    base = torch.div(src, block, rounding_mode="floor") * block
-    near = (base + torch.randint(0, block, (m,), device=device, generator=g)).clamp_(max=n - 1)
-    inside = torch.rand(m, device=device, generator=g) < p_in
-    dst = torch.where(inside, near, far)
-    del far, base, near, inside
-    keep = src != dst
-    src, dst = src[keep], dst[keep]
-    key = torch.cat([src * n + dst, dst * n + src])
-    del src, dst, keep
-    key = torch.unique(key, sorted=True)
-    row = torch.div(key, n, rounding_mode="floor")
-    col = (key - row * n).to(torch.int32)
-    del key
-    counts = torch.bincount(row, minlength=n)
-    indptr = torch.zeros(n + 1, dtype=torch.int64, device=device)
-    indptr[1:] = torch.cumsum(counts, 0)
-    return indptr.to(torch.int32), col
+    rng = np.random.default_rng(seed)
+    src = rng.integers(0, n, size=m, dtype=np.int64)
+    far = rng.integers(0, n, size=m, dtype=np.int64)
+    near = np.minimum(src // block * block + rng.integers(0, block, size=m), n - 1)
+    dst = np.where(rng.random(m) < p_in, near, far)
+    del far, near
+    return _csr_from_pairs(src, dst, n, device)
 
 
 def real_graph(name: str, device="cuda"):
     """CSR of a dataset the reference ships, standardized as its SparseGraph does."""
     import os
-
-    import numpy as np
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     d = np.load(os.path.join(root, "tests", "golden", name + ".npz"), allow_pickle=False)
@@ -144,12 +138,14 @@ def graph_for(workload: str, device="cuda"):
         return real_graph(REAL[workload], device=device)
     n, m = CONFIGS[workload][:2]
     if workload in POWERLAW:
-        return chung_lu_graph_device(n, m, SEEDS[workload], device=device)
+        return chung_lu_graph(n, m, SEEDS[workload], device=device)
     if workload in LOCAL:
-        return community_graph_device(n, m, SEEDS[workload], device=device)
-    return uniform_graph_device(n, m, SEEDS.get(workload, 0), device=device)
+        return community_graph(n, m, SEEDS[workload], device=device)
+    return uniform_graph(n, m, SEEDS.get(workload, 0), device=device)
 
 
 def features(n: int, f: int, dtype=torch.float32, device="cuda", seed: int = 0):
-    g = torch.Generator(device=device).manual_seed(seed)
-    return torch.randn(n, f, device=device, generator=g, dtype=torch.float32).to(dtype)
+    """H ~ N(0, 1): fp32 from a CPU ``torch.Generator().manual_seed(seed)``,
+    then stored as ``dtype`` on ``device``."""
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(n, f, generator=g, dtype=torch.float32).to(device=device, dtype=dtype)

@@ -31,6 +31,9 @@ def main():
     p.add_argument("--overlap", action="store_true")
     p.add_argument("--p-drop", type=float, default=0.0)
     p.add_argument("--dtype", default="f32", choices=["f32", "bf16"])
+    p.add_argument("--split", action="store_true",
+                   help="build the held rows' source-blocked copy for F (split rows) and fail "
+                        "unless the engine takes the split layout")
     a = p.parse_args()
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
@@ -52,17 +55,24 @@ def main():
     indptr, indices = synth.graph_for(a.workload, device=dev)
     H = synth.features(n, F, dtype=dtype, device=dev, seed=1)
 
-    runner = pdist.NativeRowAPPNP(indptr, indices, n, dev, overlap=a.overlap)
-    Z = runner.run(H[runner.lo:runner.hi], K, alpha, p_drop=a.p_drop, seed=5)
+    runner = pdist.NativeRowAPPNP(indptr, indices, n, dev, overlap=a.overlap,
+                                  features=F if a.split else None, dtype=dtype)
+    g = pdist._DistGraphInfo(C.c_void_p(_lib.load().appnp_dist_graph(runner._h)))
+    before = (g.source_block_layout() or {}).get("launches", 0)
+    Z = runner.run(H[runner.lo:runner.hi].contiguous(), K, alpha, p_drop=a.p_drop, seed=5)
     torch.cuda.synchronize()
+    # the split layout ran: one remainder pass per iteration (appnp_step_split)
+    split_ran = (g.source_block_layout() or {}).get("launches", 0) - before == K
+    if a.split and not split_ran:
+        print(f"[dist_capi] rank {rank}: split layout expected but not taken", flush=True)
     G = ppnp_amd.Graph.from_csr(indptr, indices, None, n, device=dev)
     ref = ppnp_amd.propagate_forward(G, H, K, alpha, p_drop=a.p_drop, seed=5)
     block = ref[runner.lo:runner.hi]
     err = (Z.double() - block.double()).abs().max().item() if block.numel() else 0.0
     scale = ref.abs().max().item()
     tol = (1e-5 if dtype == torch.float32 else 1e-2) * scale + 1e-6
-    ok = err <= tol
-    extra = ""
+    ok = err <= tol and (split_ran == a.split or runner.hi == runner.lo)
+    extra = f" split={split_ran}"
     if backend == "nccl" and world == 1:
         # the library's RCCL callback on torch's communicator: a one-rank in-place all-gather
         lib = _lib.load()
@@ -75,7 +85,7 @@ def main():
                                       C.c_void_p(comm))
         torch.cuda.synchronize()
         ok = ok and rc == 0 and torch.equal(buf, before)
-        extra = f" rccl_callback rc={rc}"
+        extra += f" rccl_callback rc={rc}"
     runner.close()
     print(f"[dist_capi] rank {rank}/{world} backend={dist.get_backend()} "
           f"exchange={runner.exchange} overlap={a.overlap} dtype={a.dtype} p_drop={a.p_drop} "

@@ -39,6 +39,8 @@ def main():
     p.add_argument("--oracle", action="store_true",
                    help="compare with the float64 CPU oracle (oracle/ppnp_oracle.py) instead of "
                         "the single-GPU HIP propagation")
+    p.add_argument("--expect-split", type=int, default=None,
+                   help="fail unless the rank's remainder columns (split rows) equal this")
     a = p.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -60,7 +62,7 @@ def main():
         a.n, a.m, a.f, a.K, a.alpha, _ = synth.CONFIGS[a.workload]
         indptr, indices = synth.graph_for(a.workload, device=dev)
     else:
-        indptr, indices = synth.uniform_graph_device(a.n, a.m, 7, device=dev)
+        indptr, indices = synth.uniform_graph(a.n, a.m, 7, device=dev)
     H = synth.features(a.n, a.f, device=dev, seed=1)
     runner = pdist.PartitionedAPPNP.create(indptr, indices, a.n, H, a.K, a.alpha, dev,
                                            layout=layout, overlap=a.overlap,
@@ -85,8 +87,11 @@ def main():
     err = (Z.double() - block.double()).abs().max().item() if block.numel() else 0.0
     tol = 1e-5 * ref.abs().max().item() + 1e-6
     ok = err <= tol
+    if a.expect_split is not None:
+        ok = ok and runner.remainder_cols == a.expect_split
     print(f"[dist_worker] rank {rank}/{world} backend={dist.get_backend()} layout={layout} "
-          f"overlap={runner.overlap} exchange={runner.exchange} rows [{runner.lo},{runner.hi}) "
+          f"overlap={runner.overlap} exchange={runner.exchange} split_cols={runner.remainder_cols} "
+          f"rows [{runner.lo},{runner.hi}) "
           f"cols [{runner.f_lo},"
           f"{runner.f_hi}) reference={'oracle' if a.oracle else 'hip'} max err {err:.3e} "
           f"tol {tol:.3e} -> {'OK' if ok else 'FAIL'}",

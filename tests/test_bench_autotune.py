@@ -1,18 +1,25 @@
-"""CPU: bench.py's multi-GPU autotune (tune_layouts) over a gloo process group of 2 ranks.
+"""CPU: bench.py's multi-GPU candidate loop (run_candidates) over a gloo process group of 2 ranks.
 
-The partitioned runner is replaced by a stub whose run() sleeps a layout-dependent time or
-raises on ONE rank, so the test pins what the driver's N > 1 bench relies on: every rank
-sees the same max-over-ranks times, picks the same layout, and a candidate that fails on any
-rank is recorded as failed and skipped on all of them (agreed over the control group) instead
-of ending the scaling run.  No GPU, no HIP library.
+The measurement of a layout is replaced by a stub that returns after a layout-dependent time,
+raises or fails parity on ONE rank, or never returns, so the test pins what the driver's N > 1
+bench relies on:
+
+* every rank sees the same max-over-ranks results and reports the same layout;
+* a candidate that fails on any rank (agreed over the control group) or fails parity is
+  recorded and skipped instead of ending the scaling run;
+* a candidate that stalls (an RCCL exchange that never completes) is ended by its deadline:
+  rank 0 still prints the line of the exchange-free layout measured first, and every rank
+  exits with status 0 instead of waiting for the process group's watchdog.
+
+No GPU, no HIP library.
 """
 
+import json
 import os
 import socket
 import time
 
 import pytest
-import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
@@ -25,83 +32,92 @@ def _free_port():
     return p
 
 
-class _StubRunner:
-    def __init__(self, tag, delay, fail):
-        self.tag, self.delay, self.fail = tag, delay, fail
-
-    def run(self):
-        if self.fail == "run":
-            raise RuntimeError(f"injected exchange failure in {self.tag}")
-        time.sleep(self.delay)
-
-
-def _worker(rank, world, port, plan, q):
+def _worker(rank, world, port, plan, out, timeout_s):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+
+    def measure(tag):
+        delay, who, what = plan[tag]
+        mine = who in (rank, "all")
+        if mine and what == "raise":
+            raise RuntimeError(f"injected exchange failure in {tag}")
+        if mine and what == "hang":
+            time.sleep(3600)
+        time.sleep(delay)
+        ok = not (mine and what == "parity")
+        return {"tag": tag, "ms_per_step": delay * 1e3, "config": {},
+                "parity": {"ok": ok}}
+
+    def emit(res):
+        with open(f"{out}.{rank}", "w") as fh:
+            fh.write(json.dumps(res))
+            fh.flush()
+            os.fsync(fh.fileno())
+
     try:
-        import bench
-        from ppnp_amd import dist as pdist
-
-        torch.cuda.synchronize = lambda *a, **k: None  # CPU: nothing queued on a device
-        torch.cuda.empty_cache = lambda: None
-
-        def create(indptr, indices, n, H, K, alpha, dev, layout, overlap, exchange):
-            tag = f"{layout.rows}x{layout.cols}-{int(overlap)}"
-            delay, fail_rank, where = plan[tag]
-            fail = where if fail_rank in (rank, "all") else None
-            if fail == "create":
-                raise RuntimeError(f"injected build failure in {tag}")
-            return _StubRunner(tag, delay, fail)
-
-        pdist.PartitionedAPPNP.create = staticmethod(create)
-        cands = [(pdist.Layout.parse(t.split("-")[0], world), t.endswith("-1"), "group")
-                 for t in plan]
-        try:
-            best, times = bench.tune_layouts(cands, None, None, 0, None, 10, 0.1, "cpu", None,
-                                             reps=2)
-            q.put((rank, best.tag, times))
-        except RuntimeError as e:
-            q.put((rank, "error", str(e)))
+        best, times = bench.run_candidates(list(plan), measure, None, timeout_s, emit,
+                                           lambda t: t, rank, world, abort=lambda: None)
+        if rank == 0:
+            emit(best)
+    except RuntimeError as e:
+        emit({"error": str(e)})
     finally:
         dist.destroy_process_group()
 
 
-def _run(plan, world=2):
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    mp.start_processes(_worker, args=(world, _free_port(), plan, q), nprocs=world, join=True,
-                       start_method="spawn")
-    return sorted(q.get() for _ in range(world))
+def _run(plan, tmp_path, world=2, timeout_s=60.0):
+    out = str(tmp_path / "line")
+    mp.start_processes(_worker, args=(world, _free_port(), plan, out, timeout_s), nprocs=world,
+                       join=True, start_method="spawn")
+    res = {}
+    for r in range(world):
+        if os.path.exists(f"{out}.{r}"):
+            res[r] = json.load(open(f"{out}.{r}"))
+    return res
 
 
-def test_autotune_agrees_and_skips_a_candidate_failing_on_one_rank():
+def test_candidates_agree_and_skip_failures(tmp_path):
     plan = {
-        "1x2-0": (0.030, None, None),    # column layout: slow
-        "2x1-1": (0.001, 1, "run"),      # row + overlap: fastest, but its exchange fails on rank 1
-        "2x1-0": (0.010, 0, "create"),   # row: fails to build on rank 0
+        "col": (0.030, None, None),      # the exchange-free layout: slow
+        "row-ov": (0.001, 1, "raise"),   # fastest, but its exchange fails on rank 1
+        "row": (0.005, 0, "parity"),     # fast, but its result is wrong on rank 0
+        "2x1": (0.010, None, None),      # the fastest that works
     }
-    res = _run(plan)
-    assert [r[0] for r in res] == [0, 1]
-    for rank, best, times in res:
-        assert best == "1x2-0", (rank, best, times)
-        assert times["rows2xcols1-overlap"] is None and times["rows2xcols1"] is None
-        assert times["rows1xcols2"] >= 30.0
-    assert res[0][2] == res[1][2]  # the same (max-over-ranks) numbers on every rank
+    res = _run(plan, tmp_path)
+    assert list(res) == [0]  # only rank 0 prints
+    line = res[0]
+    assert line["tag"] == "2x1"
+    times = line["config"]["autotune_ms_per_step"]
+    assert times["row-ov"] is None  # failed on one rank: skipped on both
+    assert times["col"] >= 30.0 and times["2x1"] >= 10.0
+    assert times["row"] is not None  # measured, but not eligible (parity)
 
 
-def test_autotune_picks_the_fastest():
-    plan = {"1x2-0": (0.030, None, None), "2x1-1": (0.005, None, None)}
-    res = _run(plan)
-    assert all(best == "2x1-1" for _, best, _ in res)
-    assert res[0][2] == res[1][2]
+def test_all_failing_raises_on_every_rank(tmp_path):
+    plan = {"col": (0.0, "all", "raise"), "row": (0.0, 0, "raise")}
+    res = _run(plan, tmp_path)
+    assert set(res) == {0, 1}
+    assert all("every candidate layout failed" in r["error"] for r in res.values())
 
 
-def test_autotune_all_failing_raises_on_every_rank():
-    plan = {"1x2-0": (0.0, "all", "create"), "2x1-1": (0.0, 0, "run")}
-    res = _run(plan)
-    assert all(best == "error" and "every candidate layout failed" in msg
-               for _, best, msg in res)
+def test_stalled_exchange_still_prints_the_column_line(tmp_path):
+    """An exchange candidate that never returns on one rank (the other waits for it in the
+    control group's agreement): both deadlines expire, rank 0 prints the column layout's line
+    with the stalled candidate marked, and both processes exit 0 (start_processes raises
+    otherwise)."""
+    plan = {"col": (0.02, None, None), "2x4-multipath": (0.0, 1, "hang"),
+            "never": (0.0, None, None)}
+    t0 = time.time()
+    res = _run(plan, tmp_path, timeout_s=4.0)
+    assert time.time() - t0 < 60
+    assert list(res) == [0]
+    line = res[0]
+    assert line["tag"] == "col"
+    times = line["config"]["autotune_ms_per_step"]
+    assert times["2x4-multipath"] == "timeout" and times["col"] >= 20.0
+    assert "never" not in times
 
 
 if __name__ == "__main__":

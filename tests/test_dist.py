@@ -132,6 +132,15 @@ def test_layout_helpers():
     c8 = candidate_layouts(8, 100)
     assert c8[0] == (Layout(1, 8), False, "group") and (Layout(2, 4), True, "multipath") in c8
     assert (Layout(8, 1), True, "group") in c8 and (Layout(8, 1), True, "native") in c8
+    # both 2-D layouts the single-GPU emulation priced (2x4 1.24 ms, 4x2 1.21 ms
+    # per rank-iteration), each with both exchanges; the exchange-free column layout first
+    for lay in (Layout(2, 4), Layout(4, 2)):
+        assert (lay, True, "multipath") in c8 and (lay, True, "group") in c8
+    assert len(c8) == len(set(c8)) == 7
+    c4 = candidate_layouts(4, 100)
+    assert c4 == [(Layout(1, 4), False, "group"), (Layout(2, 2), True, "multipath"),
+                  (Layout(2, 2), True, "group"), (Layout(4, 1), True, "group"),
+                  (Layout(4, 1), True, "native")]
 
 
 def test_layout_memory_and_index_limits():

@@ -96,9 +96,10 @@ def _products_case(name):
     rp, col, val, _ = G.csr()
     a = torch.sparse_csr_tensor(rp.cpu().long(), col.cpu().long(), val.cpu().double(),
                                 size=(n, n))
+    adj = _adj(indptr, indices, n)
     del rp, col, val, indices
     torch.set_num_threads(max(1, min(16, len(os.sched_getaffinity(0)))))
-    return G, H, K, alpha, a
+    return G, H, K, alpha, a, adj
 
 
 def _check_full(got, ref):
@@ -109,9 +110,28 @@ def _check_full(got, ref):
 
 @pytest.fixture(scope="module")
 def products():
-    G, H, K, alpha, a = _products_case("products-synth")
-    yield G, H, K, alpha, a
+    G, H, K, alpha, a, adj = _products_case("products-synth")
+    yield G, H, K, alpha, a, adj
     G.close()
+
+
+def test_products_a_hat_matches_calc_a_hat(products):
+    """The device CSR build at products scale (126 M entries of A_hat) against the oracle's
+    calc_a_hat (helpers.py:58-66) on the same A: row pointers and column indices bit-exact,
+    values equal to float32 of the fp64 reference, every entry (pinned so far only
+    up to arxiv size)."""
+    G, _, _, _, _, adj = products
+    ref = O.calc_a_hat(adj, "sym")
+    rp, col, val, dinv = G.csr()
+    assert np.array_equal(rp.cpu().numpy().astype(np.int64), ref.indptr.astype(np.int64))
+    col = col.cpu().numpy()
+    assert np.array_equal(col, ref.indices.astype(np.int32))
+    del col
+    assert np.array_equal(val.cpu().numpy(), ref.data.astype(np.float32))
+    # the fp64 degree scale the build keeps: 1/sqrt(D), D the weighted row sum of A + I
+    deg = np.diff(adj.indptr).astype(np.float64) + 1.0
+    rel = np.abs(dinv.cpu().numpy() * np.sqrt(deg) - 1.0).max()
+    assert rel <= 2.0 ** -51, rel
 
 
 def test_products_k10_matches_oracle(products):
@@ -119,7 +139,7 @@ def test_products_k10_matches_oracle(products):
     against the float64 torch.sparse CPU loop of the same A_hat (helpers.py:58-66)."""
     import ppnp_amd
 
-    G, H, K, alpha, a = products
+    G, H, K, alpha, a, _ = products
     Z = ppnp_amd.propagate_forward(G, H, K, alpha).cpu()
     _check_full(Z, O.appnp_propagate_torch_cpu(a, H.cpu().double(), K, alpha))
 
@@ -130,7 +150,7 @@ def test_products_k10_backward_matches_oracle(products):
     the symmetric A_hat, so J^T dZ = APPNP_K(dZ): the float64 forward loop is its oracle."""
     import ppnp_amd
 
-    G, H, K, alpha, a = products
+    G, H, K, alpha, a, _ = products
     g = torch.Generator(device="cpu").manual_seed(11)
     dZ = torch.randn(H.shape, generator=g, dtype=torch.float32)
     dH = ppnp_amd.propagate_backward(G, dZ.to(DEV), K, alpha).cpu()
@@ -142,7 +162,7 @@ def test_products_k10_bf16_matches_oracle(products):
     is fp32-only), against the float64 loop on the bf16-rounded H: the bf16 bar of DESIGN.md 2."""
     import ppnp_amd
 
-    G, H, K, alpha, a = products
+    G, H, K, alpha, a, _ = products
     Hb = H.to(torch.bfloat16)
     assert G.split_point(int(H.shape[1]), torch.bfloat16) == 0
     Z = ppnp_amd.propagate_forward(G, Hb, K, alpha).float().cpu().double()
@@ -156,7 +176,7 @@ def test_products_powerlaw_k10_matches_oracle():
     hub lists of the main SpMM and long runs in the remainder pass) at full size, K = 10."""
     import ppnp_amd
 
-    G, H, K, alpha, a = _products_case("products-powerlaw")
+    G, H, K, alpha, a, _ = _products_case("products-powerlaw")
     try:
         Z = ppnp_amd.propagate_forward(G, H, K, alpha).cpu()
     finally:
@@ -261,3 +281,41 @@ def test_native_row_engine_rccl_callback_one_rank():
     lines = [l for l in proc.stdout.splitlines() if l.startswith("[dist_capi]")]
     assert proc.returncode == 0, proc.stdout[-3000:] + proc.stderr[-3000:]
     assert len(lines) == 1 and "rccl_callback rc=0" in lines[0] and lines[0].endswith("OK"), lines
+
+
+@pytest.mark.parametrize("ranks,extra", [(2, []), (2, ["--overlap"]),
+                                         (3, ["--overlap", "--p-drop", "0.3"])])
+def test_row_partition_split_rows_matches_oracle(ranks, extra):
+    """the north_star's row partition at F = 100 on a graph above 2^16 nodes
+    takes the split layout on every rank (appnp_step_split: 3 gathered lines of the 96 main
+    columns, the L2-blocked pass for the last 4, both parts exchanged), with and without the
+    overlapped local/remote split and with dropout; each rank's block against the float64
+    oracle."""
+    env = dict(os.environ, PPNP_DIST_BACKEND="gloo", PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={ranks}", "--master-addr=127.0.0.1",
+           f"--master-port={_free_port()}", os.path.join(ROOT, "tests", "dist_worker.py"),
+           "--layout", "row", "--n", "200000", "--m", "1000000", "--f", "100", "--K", "4",
+           "--oracle", "--expect-split", "4", *extra]
+    proc = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=150)
+    lines = [l for l in proc.stdout.splitlines() if l.startswith("[dist_worker]")]
+    assert proc.returncode == 0, proc.stdout[-3000:] + proc.stderr[-3000:]
+    assert len(lines) == ranks and all(l.endswith("OK") for l in lines), lines
+
+
+@pytest.mark.parametrize("ranks,extra", [(2, []), (2, ["--overlap", "--p-drop", "0.3"]),
+                                         (3, ["--overlap"])])
+def test_native_row_engine_split_rows(ranks, extra):
+    """The library's own row loop (appnp_dist_propagate) on the split layout: arxiv-synth's
+    graph at F = 100, every rank's held rows with their own source-blocked copy, both parts
+    exchanged through the callback, against the single-GPU appnp_propagate."""
+    env = dict(os.environ, PPNP_DIST_BACKEND="gloo", PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={ranks}", "--master-addr=127.0.0.1",
+           f"--master-port={_free_port()}", os.path.join(ROOT, "tests", "dist_capi_worker.py"),
+           "--workload", "arxiv-synth", "--features", "100", "--split", *extra]
+    proc = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=150)
+    lines = [l for l in proc.stdout.splitlines() if l.startswith("[dist_capi]")]
+    assert proc.returncode == 0, proc.stdout[-3000:] + proc.stderr[-3000:]
+    assert len(lines) == ranks and all("split=True" in l and l.endswith("OK") for l in lines), \
+        lines

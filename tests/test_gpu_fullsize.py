@@ -24,7 +24,7 @@ def products():
     from ppnp_amd import synth
 
     n, m, F, K, alpha, _ = synth.CONFIGS["products-synth"]
-    indptr, indices = synth.uniform_graph_device(n, m, synth.SEEDS["products-synth"], device=DEV)
+    indptr, indices = synth.uniform_graph(n, m, synth.SEEDS["products-synth"], device=DEV)
     return dict(n=n, F=F, K=K, alpha=alpha, indptr=indptr, indices=indices)
 
 

@@ -151,7 +151,7 @@ def test_split_point_follows_gather_locality(graphs):
     assert graphs[0].split_point(128) == 0 and graphs[0].split_point(101) == 0
     assert graphs[0].split_point(100, torch.bfloat16) == 0
     assert graphs[1].split_point(100) == 0  # built without source blocks
-    ip, ix = synth.community_graph_device(N, 1_500_000, 7, device=DEV)
+    ip, ix = synth.community_graph(N, 1_500_000, 7, device=DEV)
     local = ppnp_amd.Graph.from_csr(ip, ix, None, N, device=DEV, source_blocks=True)
     assert local.split_point(100) == 0
 
@@ -329,7 +329,10 @@ def test_wide_remainder_matches_oracle(wide, ahat, w, f, K):
     Hb = torch.zeros(N, ld, device=DEV)
     Hb[:, :f] = H.to(DEV)
     Zb = torch.empty(N, ld, device=DEV)
+    before = G.source_block_layout()["launches"]
     Z = ppnp_amd.propagate_forward(G, Hb[:, :f], K, 0.1, out=Zb[:, :f])
+    # the path taken, not just the one reported: K remainder launches iff the split applies
+    assert G.source_block_layout()["launches"] - before == (K if r else 0)
     close_fp32(Z.double().cpu().numpy(), O.appnp_propagate(ahat, H.numpy(), K, 0.1))
     Z2 = ppnp_amd.propagate_forward(G, Hb[:, :f], K, 0.1, out=torch.empty_like(Zb)[:, :f])
     assert torch.equal(Z, Z2)  # deterministic
@@ -407,9 +410,63 @@ def test_narrow_rows_on_the_four_column_layout(graphs, ahat, f):
     Hb = torch.zeros(N, 4, device=DEV)
     Hb[:, :f] = H.to(DEV)
     Zb = torch.full((N, 4), 9.0, device=DEV)
+    before = G.source_block_layout()["launches"]
     Z = ppnp_amd.propagate_forward(G, Hb[:, :f], 3, 0.1, out=Zb[:, :f])
+    assert G.source_block_layout()["launches"] - before == 3  # ran in the pass
     close_fp32(Z.double().cpu().numpy(), O.appnp_propagate(ahat, H.numpy(), 3, 0.1))
     assert bool((Zb[:, f:] == 9.0).all())
+    # a packed [N, f] H of f < 4 columns has no 16-B rows: whole rows, reported as such
+    Hp = H.to(DEV).contiguous()
+    before = G.source_block_layout()["launches"]
+    Zp = ppnp_amd.propagate_forward(G, Hp, 3, 0.1)
+    assert G.source_block_layout()["launches"] - before == (3 if f == 4 else 0)
+    close_fp32(Zp.double().cpu().numpy(), O.appnp_propagate(ahat, H.numpy(), 3, 0.1))
     if f == 4:  # the adjoint makes dZ contiguous: ld 4 keeps the 16-B vectors
         dH = ppnp_amd.propagate_backward(G, H.to(DEV), 3, 0.1)
         close_fp32(dH.double().cpu().numpy(), O.appnp_backward(ahat, H.numpy(), 3, 0.1))
+
+
+def test_source_blocks_enomem_leaves_no_stale_error(monkeypatch, ahat):
+    """a regrouped copy whose allocation really fails (APPNP_SB_TEST_OOM asks for
+    2^60 bytes) is tolerated -- the graph is created without it, warns, and the failed
+    hipMalloc's error is cleared, so the first propagation and an unrelated torch kernel both
+    succeed."""
+    import ppnp_amd
+
+    monkeypatch.setenv("APPNP_SB_TEST_OOM", "1")
+    with pytest.warns(RuntimeWarning, match="could not be built"):
+        G = ppnp_amd.Graph.from_csr(ahat.indptr, ahat.indices, None, N, device=DEV,
+                                    source_blocks=True)
+    monkeypatch.delenv("APPNP_SB_TEST_OOM")
+    assert G.source_block_layout() is None and G.remainder_cols(100) == 0
+    H = _h(100, 37).to(DEV)
+    Z = ppnp_amd.propagate_forward(G, H, 3, 0.1)
+    x = torch.arange(1 << 20, device=DEV, dtype=torch.float32).sum()
+    torch.cuda.synchronize()
+    assert torch.isfinite(Z).all() and float(x) > 0
+
+
+def test_workspace_covers_the_wide_split_layout(wide):
+    """appnp_workspace_bytes counts the split buffers of a W8 / W16 copy ([n, fs] +
+    [n, 4 LPE] each), which are wider than a packed narrow row, so the split path runs from a
+    workspace of exactly that size instead of silently falling back to whole rows."""
+    import ctypes as C
+
+    from ppnp_amd import _lib
+
+    lib = _lib.load()
+    for w, f in ((16, 8), (16, 4), (8, 4), (16, 13)):
+        G = wide[w]
+        ws = int(lib.appnp_workspace_bytes(G.handle, f, f, _lib.F32))
+        buf = ((N * 16 * (w // 4) + 255) // 256) * 256  # fs = 0: the remainder part only
+        assert ws >= 2 * buf, (w, f, ws, buf)
+        H = torch.zeros(N, 4 * ((f + 3) // 4), device=DEV)[:, :f]
+        Z = torch.empty_like(H)
+        wsb = torch.empty(ws, dtype=torch.uint8, device=DEV)
+        before = G.source_block_layout()["launches"]
+        rc = lib.appnp_propagate(G.handle, C.c_void_p(H.data_ptr()), H.stride(0),
+                                 C.c_void_p(Z.data_ptr()), Z.stride(0), f, _lib.F32, 2, 0.1,
+                                 0.0, 0, C.c_void_p(wsb.data_ptr()), ws,
+                                 C.c_void_p(torch.cuda.current_stream().cuda_stream))
+        assert rc == 0
+        assert G.source_block_layout()["launches"] - before == 2, (w, f)

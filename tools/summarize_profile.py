@@ -109,7 +109,10 @@ def main():
                 summ["bench"] = json.loads(line)
     if "bench" in summ:
         b = summ["bench"]
-        key = f"{b['config']['workload']}:{b['dtype']}:{b['config']['parallelism']}"
+        # the bench's own key: workload, dtype, layout, the iteration's kernels and a digest of
+        # the kernel sources, so a profile of other or older kernels never matches a run
+        key = b["roofline"].get("traffic_key") or (
+            f"{b['config']['workload']}:{b['dtype']}:{b['config']['parallelism']}")
         tpath = os.path.join(prof, "pmc_traffic.json")
         table = json.load(open(tpath)) if os.path.exists(tpath) else {}
         table[key] = fetch_b + write_b
