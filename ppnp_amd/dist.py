@@ -721,6 +721,7 @@ class NativeRowRunner:
         self.rank = self.engine.rank
         self.overlap = bool(overlap and self.engine.world > 1)
         self.lo, self.hi = self.engine.lo, self.engine.hi
+        self.shard = self.engine.shard
         self.f_lo, self.f_hi = 0, int(H.shape[1])
         self.H = H[self.lo:self.hi].to(device).contiguous()
         self.K, self.alpha, self.p_drop, self.seed = K, alpha, p_drop, seed

@@ -2,7 +2,8 @@
 """End-to-end check of the multi-GPU path on real HIP kernels.
 
     torchrun --nproc-per-node P --master-addr 127.0.0.1 tests/dist_worker.py --layout row|col|RxC
-        [--overlap] [--exchange multipath|group] [--n 60000] [--m 400000] [--f 20] [--K 10]
+        [--overlap] [--exchange multipath|group] [--graph-n 60000] [--graph-m 400000] [--f 20]
+        [--K 10]
         [--p-drop 0.0] [--workload arxiv-synth] [--oracle]
 
 Every rank runs its share (ppnp_amd.dist.PartitionedAPPNP) and compares its block of Z_K with
@@ -27,8 +28,9 @@ def main():
     p.add_argument("--layout", default="col")
     p.add_argument("--overlap", action="store_true")
     p.add_argument("--exchange", default="multipath", choices=["multipath", "group"])
-    p.add_argument("--n", type=int, default=60000)
-    p.add_argument("--m", type=int, default=400000)
+    # not --n / --m: torch.distributed.run would take them as abbreviations of its own options
+    p.add_argument("--graph-n", dest="n", type=int, default=60000)
+    p.add_argument("--graph-m", dest="m", type=int, default=400000)
     p.add_argument("--f", type=int, default=20)
     p.add_argument("--K", type=int, default=10)
     p.add_argument("--alpha", type=float, default=0.1)

@@ -206,7 +206,7 @@ def test_arxiv_row_partition_matches_oracle(ranks, extra):
     proc = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=110)
     lines = [l for l in proc.stdout.splitlines() if l.startswith("[dist_worker]")]
     assert proc.returncode == 0, proc.stdout[-3000:] + proc.stderr[-3000:]
-    assert len(lines) == ranks and all(l.endswith("OK") for l in lines), lines
+    assert len(lines) == ranks and all(l.endswith("OK") for l in lines), proc.stdout[-4000:]
 
 
 def test_stream_done_orders_consumer_after_side_stream():
@@ -266,7 +266,7 @@ def test_native_row_engine_matches_single_gpu(ranks, extra):
     proc = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=110)
     lines = [l for l in proc.stdout.splitlines() if l.startswith("[dist_capi]")]
     assert proc.returncode == 0, proc.stdout[-3000:] + proc.stderr[-3000:]
-    assert len(lines) == ranks and all(l.endswith("OK") for l in lines), lines
+    assert len(lines) == ranks and all(l.endswith("OK") for l in lines), proc.stdout[-4000:]
 
 
 def test_native_row_engine_rccl_callback_one_rank():
@@ -295,12 +295,13 @@ def test_row_partition_split_rows_matches_oracle(ranks, extra):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
            f"--nproc-per-node={ranks}", "--master-addr=127.0.0.1",
            f"--master-port={_free_port()}", os.path.join(ROOT, "tests", "dist_worker.py"),
-           "--layout", "row", "--n", "200000", "--m", "1000000", "--f", "100", "--K", "4",
+           "--layout", "row", "--graph-n", "200000", "--graph-m", "1000000", "--f", "100",
+           "--K", "4",
            "--oracle", "--expect-split", "4", *extra]
     proc = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=150)
     lines = [l for l in proc.stdout.splitlines() if l.startswith("[dist_worker]")]
     assert proc.returncode == 0, proc.stdout[-3000:] + proc.stderr[-3000:]
-    assert len(lines) == ranks and all(l.endswith("OK") for l in lines), lines
+    assert len(lines) == ranks and all(l.endswith("OK") for l in lines), proc.stdout[-4000:]
 
 
 @pytest.mark.parametrize("ranks,extra", [(2, []), (2, ["--overlap", "--p-drop", "0.3"]),

@@ -461,7 +461,7 @@ def test_workspace_covers_the_wide_split_layout(wide):
         buf = ((N * 16 * (w // 4) + 255) // 256) * 256  # fs = 0: the remainder part only
         assert ws >= 2 * buf, (w, f, ws, buf)
         H = torch.zeros(N, 4 * ((f + 3) // 4), device=DEV)[:, :f]
-        Z = torch.empty_like(H)
+        Z = torch.empty(N, 4 * ((f + 3) // 4), device=DEV)[:, :f]
         wsb = torch.empty(ws, dtype=torch.uint8, device=DEV)
         before = G.source_block_layout()["launches"]
         rc = lib.appnp_propagate(G.handle, C.c_void_p(H.data_ptr()), H.stride(0),
