@@ -56,6 +56,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip-level param
 GATHER_LINE_CEILING = 60.0
 # xGMI: 7 links per GPU at 76.8 GB/s per direction (153.6 GB/s bidirectional)
 XGMI_IN_GBS = 7 * 76.8
+# L2 read bandwidth, all XCDs (MI355X_MICROARCH.md "L2 (per XCD)": ~34.5 TB/s): bounds the
+# remainder pass, whose gathers are L2 requests
+L2_PEAK_GBS = 34500.0
 
 
 def parse(argv=None):
@@ -220,14 +223,17 @@ def roofline(*, n, rows, nnz, F_local, esz, avg_iter_ms, fs, r, lpe, rb_total=0,
     rank's A_hat rows once, all n rows of its slab of Z_k once (a row-layout rank gathers every
     row), H and Z_{k+1} of its rows once.  For one GPU this is SURVEY 8(d)'s 4(N+1)+8nnz+3NFs.
 
-    ceiling = the iteration's line requests beyond L2 at the fastest measured random-line rate:
-    ``lines_per_nonzero`` gathered 128-B lines per nonzero of the SpMM kernel (whole lines of the
-    fs main columns, or all of a whole row), plus every streamed byte (CSR, the remainder pass's
-    regrouped entries, H, Z) / 128; the remainder pass's gathers are L2 requests and are not
-    counted.  A row layout's exchange adds max(compute bound, exchange bytes / xGMI link peak).
-    A lower bound on the time, so ceiling.frac >= frac on a uniform random graph; a graph with
-    gather locality (L2 hits) can beat it, and then the ceiling is clamped to the measured time
-    and says so."""
+    ceiling = a lower bound on the iteration time, the largest of
+      * the line requests beyond L2 at the fastest measured random-line rate --
+        ``lines_per_nonzero`` gathered 128-B lines per nonzero of the SpMM kernel (whole lines
+        of the fs main columns, or all of a whole row) plus every streamed byte (CSR, the
+        remainder pass's regrouped entries, H, Z) / 128 -- plus the remainder pass's gathers
+        (16 B x lanes per entry, L2 requests) at the L2's peak bandwidth;
+      * a row layout's exchange: the bytes landing here / the xGMI links' peak;
+      * B_iter at the HBM peak (the roofline itself), so ceiling.frac <= 1.
+    So frac <= ceiling.frac <= 1 on a uniform random graph; a graph with gather locality (L2
+    hits) can beat the line bound, and then the ceiling is clamped to the measured time and
+    says so."""
     from ppnp_amd.dist import _avg_lines, line_ld
 
     s = esz
@@ -245,9 +251,11 @@ def roofline(*, n, rows, nnz, F_local, esz, avg_iter_ms, fs, r, lpe, rb_total=0,
         ld_main = ld
         dense = 2 * rows * ld_main * s
     lines = nnz * lpn + (stream + dense) / 128
-    compute_ms = lines / (GATHER_LINE_CEILING * 1e9) * 1e3
+    l2_bytes = nnz * 16 * lpe if r else 0
+    compute_ms = (lines / (GATHER_LINE_CEILING * 1e9) + l2_bytes / (L2_PEAK_GBS * 1e9)) * 1e3
     exchange_ms = exchange_in_bytes / (XGMI_IN_GBS * 1e9) * 1e3
-    ceil_ms = max(compute_ms, exchange_ms)
+    hbm_ms = b_iter / (HBM_PEAK_GBS * 1e9) * 1e3
+    ceil_ms = max(compute_ms, exchange_ms, hbm_ms)
     note = ("a uniform random graph gathers whole cache lines per nonzero, so the "
             "compulsory-byte fraction is capped at ceiling.frac; 60 % of the compulsory-byte "
             "roofline is out of reach for it on one GPU")
@@ -288,11 +296,15 @@ def roofline(*, n, rows, nnz, F_local, esz, avg_iter_ms, fs, r, lpe, rb_total=0,
             "remainder_l2_requests_per_nonzero": lpe if r else 0,
             "compute_ms": compute_ms,
             "exchange_ms": exchange_ms,
+            "hbm_ms": hbm_ms,
+            "remainder_l2_bytes": l2_bytes,
             "exchange_in_bytes": exchange_in_bytes,
             "clamped_to_measured": clamped,
-            "basis": f"{lines:.4g} line requests per iteration at {GATHER_LINE_CEILING} G "
-                     f"lines/s; exchange {exchange_in_bytes / 1e6:.4g} MB in at "
-                     f"{XGMI_IN_GBS:.0f} GB/s",
+            "basis": f"max of: {lines:.4g} line requests per iteration at "
+                     f"{GATHER_LINE_CEILING} G lines/s + {l2_bytes / 1e9:.4g} GB of remainder "
+                     f"gathers at the {L2_PEAK_GBS / 1e3:.1f} TB/s L2 peak; exchange "
+                     f"{exchange_in_bytes / 1e6:.4g} MB in at {XGMI_IN_GBS:.0f} GB/s; B_iter at "
+                     f"the HBM peak",
         },
         "note": note,
     }

@@ -12,6 +12,9 @@
  *                                            launches  Z <- (1-a) A_hat Z + a H
  *   appnp_propagate_bwd   model.py:63        autograd of the same product (dH = J^T dZ)
  *   appnp_step            one iteration; used by the row-partitioned multi-GPU driver
+ *   appnp_step_split      the same on the split layout (whole-line main columns + the
+ *                         L2-blocked remainder pass) of a row-partitioned graph
+ *   appnp_dist_*          the row partition's whole K loop (SURVEY.md 8(b) appnp_dist_create)
  *   appnp_standardize     ppnp/data/sparsegraph.py:191-222  SparseGraph.standardize
  *                         (unweighted, undirected, no self loops, largest CC)
  *   appnp_spmm            model.py:36-38,47  Dropout + X @ W1 of the encoder on a CSR X

@@ -66,9 +66,9 @@
 namespace appnp {
 namespace {
 
-constexpr int kRemThreads = kRemWaves * kWave;  // 1024
+constexpr int kRemThreads = kRemWaves * kWave;  // 1024 at 16 waves
 constexpr int kRemLdsBytes = 160 * 1024;        // LDS per CU on gfx950
-constexpr int kRemMaxRg = kRemLdsBytes / (kRemWaves * 16);  // 640 rows per wave group
+constexpr int kRemMaxRg = kRemLdsBytes / (kRemWaves * 16);  // 640 rows per wave group at 16
 constexpr uint32_t kRemNone = 0xffffffffu;      // packed entry of an idle lane (row 4095)
 constexpr int kWalkWaves = kWavesPerBlock;      // build walk: one wave per group
 constexpr int kWalkMaxBlocks = 4096;            // LDS cursors of the build walk: 64 KiB

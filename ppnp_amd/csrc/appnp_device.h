@@ -61,7 +61,10 @@ constexpr int kSourceBlockLog2 = 15;  // source rows per block of the remainder 
                                      // over a few blocks, which must share its 4 MB L2:
                                      // products-synth 2^14 / 2^15 / 2^16 / 2^17 rows
                                      // 8.00 / 7.97 / 8.22 / 8.27 ms per iteration)
-constexpr int kRemWaves = 16;        // waves per workgroup of the persistent remainder pass
+#ifndef APPNP_REM_WAVES
+#define APPNP_REM_WAVES 16  // -DAPPNP_REM_WAVES=n: measurement variants (tools/build_variant.sh)
+#endif
+constexpr int kRemWaves = APPNP_REM_WAVES;  // waves per workgroup of the persistent remainder pass
 constexpr int kRemColBits = 20;      // column-in-block bits of a packed remainder entry
 constexpr int kRemRowBits = 12;      // row-in-group bits (the rest of the 32)
 constexpr int kNearRows = 1 << 14;  // "near" entry: |col - row| below this (gather locality)
