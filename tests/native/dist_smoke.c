@@ -5,8 +5,12 @@
  * appnp_dist handle, and the exchange callback is an in-process all-gather: drain the stream,
  * barrier, copy every peer's shard out of the peer's buffer, drain, barrier.  Each rank's rows
  * of Z_K are compared with appnp_propagate of the whole graph.  Cases: overlap (local columns
- * while the exchange runs) and plain, with and without edge dropout.  Built by
- * tests/test_native.py with gcc; run on the GPU box.  Exit status 0 on success.
+ * while the exchange runs) and plain, with and without edge dropout, on two graphs: 3,001 nodes
+ * at F = 12 (whole rows), and 300,001 nodes at F = 100 with APPNP_GRAPH_SOURCE_BLOCKS in `mode`,
+ * where every rank's held rows run the split layout (appnp_step_split: 96 gathered columns + the
+ * L2-blocked remainder pass, both parts exchanged) -- checked through the remainder-pass launch
+ * counter of each rank's graph.  Built by tests/test_native.py with gcc; run on the GPU box.
+ * Exit status 0 on success.
  */
 #define _POSIX_C_SOURCE 200809L
 #include <hip/hip_runtime_api.h>
@@ -18,7 +22,7 @@
 
 #include "ppnp_amd.h"
 
-enum { P = 2, N = 3001, F = 12, K = 10, DEG = 4 };
+enum { P = 2, K = 10, DEG = 4 };
 
 struct world {
   pthread_barrier_t bar;
@@ -27,6 +31,8 @@ struct world {
 
 struct rank_ctx {
   struct world* w;
+  int64_t N, F;
+  int mode;  /* APPNP_NORM_SYM, | APPNP_GRAPH_SOURCE_BLOCKS for the split case */
   int rank, overlap;
   float p_drop;
   const int32_t *d_ip, *d_ix;
@@ -35,6 +41,7 @@ struct rank_ctx {
   float* d_Zref;    /* single-GPU result */
   int rc;
   double err;
+  int64_t rem_launches; /* remainder passes this rank's propagation enqueued */
 };
 
 static int exchange(void* buf, size_t shard_bytes, int rank, int nranks, void* stream,
@@ -58,12 +65,13 @@ static int exchange(void* buf, size_t shard_bytes, int rank, int nranks, void* s
 
 static void* run_rank(void* arg) {
   struct rank_ctx* c = (struct rank_ctx*)arg;
+  const int64_t N = c->N, F = c->F;
   hipStream_t s;
   appnp_dist* d = NULL;
   c->rc = -1;
   if (hipStreamCreate(&s) != hipSuccess) return NULL;
-  int rc = appnp_dist_create(c->d_ip, c->d_ix, NULL, N, c->nnz, APPNP_NORM_SYM, c->rank, P,
-                             c->overlap, exchange, c->w, s, &d);
+  int rc = appnp_dist_create(c->d_ip, c->d_ix, NULL, N, c->nnz, c->mode, c->rank, P, c->overlap,
+                             exchange, c->w, s, &d);
   if (rc != APPNP_OK) { c->rc = rc; return NULL; }
   int64_t lo, hi, shard;
   appnp_dist_rows(d, &lo, &hi, &shard);
@@ -75,9 +83,13 @@ static void* run_rank(void* arg) {
     c->rc = APPNP_ENOMEM;
     return NULL;
   }
+  int64_t before = 0, after = 0;
+  appnp_graph_source_block_layout(appnp_dist_graph(d), NULL, NULL, NULL, NULL, &before);
   rc = appnp_dist_propagate(d, c->d_H + lo * F, F, d_Z, F, F, APPNP_F32, K, 0.1f, c->p_drop, 77,
                             ws, ws_bytes, s);
   if (rc == APPNP_OK && hipStreamSynchronize(s) != hipSuccess) rc = APPNP_EDEVICE;
+  appnp_graph_source_block_layout(appnp_dist_graph(d), NULL, NULL, NULL, NULL, &after);
+  c->rem_launches = after - before;
   if (rc == APPNP_OK) {
     const size_t cnt = (size_t)(hi - lo) * F;
     float* z = (float*)malloc(cnt * 4);
@@ -98,58 +110,62 @@ static void* run_rank(void* arg) {
   return NULL;
 }
 
-int main(void) {
-  /* a ring plus DEG-2 pseudo-random chords per node, symmetrised, sorted */
-  static int32_t adj[N][2 * DEG];
-  static int cnt[N];
+/* One graph: n nodes, a ring plus DEG-2 pseudo-random chords per node, symmetrised, sorted;
+ * F features; sb != 0 builds every rank's source-blocked copy (split rows).  Returns the number
+ * of failed (overlap, p_drop) cases, or a negative setup error. */
+static int run_case(const int64_t N, const int64_t F, const int sb) {
+  int32_t* adj = (int32_t*)malloc((size_t)N * 2 * DEG * 4);
+  int* cnt = (int*)calloc((size_t)N, sizeof(int));
   unsigned long long st = 12345;
-  for (int i = 0; i < N; ++i) {
-    int js[DEG];
+  for (int64_t i = 0; i < N; ++i) {
+    int64_t js[DEG];
     js[0] = (i + 1) % N;
     for (int t = 1; t < DEG - 1; ++t) {
       st = st * 6364136223846793005ull + 1442695040888963407ull;
-      js[t] = (int)((st >> 33) % N);
+      js[t] = (int64_t)((st >> 33) % (unsigned long long)N);
     }
     for (int t = 0; t < DEG - 1; ++t) {
-      const int j = js[t];
+      const int64_t j = js[t];
       if (j == i) continue;
       int dup = 0;
-      for (int q = 0; q < cnt[i]; ++q) dup |= adj[i][q] == j;
+      for (int q = 0; q < cnt[i]; ++q) dup |= adj[i * 2 * DEG + q] == j;
       if (dup || cnt[i] >= 2 * DEG || cnt[j] >= 2 * DEG) continue;
-      adj[i][cnt[i]++] = j;
-      adj[j][cnt[j]++] = i;
+      adj[i * 2 * DEG + cnt[i]++] = (int32_t)j;
+      adj[j * 2 * DEG + cnt[j]++] = (int32_t)i;
     }
   }
-  int32_t* indptr = (int32_t*)malloc((N + 1) * 4);
+  int32_t* indptr = (int32_t*)malloc((size_t)(N + 1) * 4);
   int32_t* indices = (int32_t*)malloc((size_t)N * 2 * DEG * 4);
   int64_t nnz = 0;
-  for (int i = 0; i < N; ++i) {
+  for (int64_t i = 0; i < N; ++i) {
+    int32_t* row = adj + i * 2 * DEG;
     indptr[i] = (int32_t)nnz;
     for (int a = 1; a < cnt[i]; ++a)  /* insertion sort of the row */
-      for (int b = a; b > 0 && adj[i][b - 1] > adj[i][b]; --b) {
-        const int32_t t = adj[i][b];
-        adj[i][b] = adj[i][b - 1];
-        adj[i][b - 1] = t;
+      for (int b = a; b > 0 && row[b - 1] > row[b]; --b) {
+        const int32_t t = row[b];
+        row[b] = row[b - 1];
+        row[b - 1] = t;
       }
-    for (int a = 0; a < cnt[i]; ++a) indices[nnz++] = adj[i][a];
+    for (int a = 0; a < cnt[i]; ++a) indices[nnz++] = row[a];
   }
   indptr[N] = (int32_t)nnz;
   float* H = (float*)malloc((size_t)N * F * 4);
-  for (int i = 0; i < N * F; ++i) H[i] = (float)((i * 7919) % 2001 - 1000) / 1000.0f;
+  for (int64_t i = 0; i < N * F; ++i) H[i] = (float)((i * 7919) % 2001 - 1000) / 1000.0f;
 
   int32_t *d_ip, *d_ix;
   float *d_H, *d_Zref;
   void* d_ws;
-  if (hipMalloc((void**)&d_ip, (N + 1) * 4) || hipMalloc((void**)&d_ix, nnz * 4) ||
+  if (hipMalloc((void**)&d_ip, (size_t)(N + 1) * 4) || hipMalloc((void**)&d_ix, nnz * 4) ||
       hipMalloc((void**)&d_H, (size_t)N * F * 4) || hipMalloc((void**)&d_Zref, (size_t)N * F * 4))
-    return 2;
-  hipMemcpy(d_ip, indptr, (N + 1) * 4, hipMemcpyHostToDevice);
+    return -2;
+  hipMemcpy(d_ip, indptr, (size_t)(N + 1) * 4, hipMemcpyHostToDevice);
   hipMemcpy(d_ix, indices, nnz * 4, hipMemcpyHostToDevice);
   hipMemcpy(d_H, H, (size_t)N * F * 4, hipMemcpyHostToDevice);
+  const int mode = APPNP_NORM_SYM | (sb ? APPNP_GRAPH_SOURCE_BLOCKS : 0);
   appnp_graph* g = NULL;
-  if (appnp_graph_create(d_ip, d_ix, NULL, N, nnz, APPNP_NORM_SYM, NULL, &g) != APPNP_OK) return 3;
+  if (appnp_graph_create(d_ip, d_ix, NULL, N, nnz, mode, NULL, &g) != APPNP_OK) return -3;
   const size_t ws_bytes = appnp_workspace_bytes(g, F, F, APPNP_F32);
-  if (hipMalloc(&d_ws, ws_bytes ? ws_bytes : 1)) return 2;
+  if (hipMalloc(&d_ws, ws_bytes ? ws_bytes : 1)) return -2;
 
   int failures = 0;
   const float drops[2] = {0.0f, 0.25f};
@@ -158,22 +174,27 @@ int main(void) {
       if (appnp_propagate(g, d_H, F, d_Zref, F, F, APPNP_F32, K, 0.1f, drops[di], 77, d_ws,
                           ws_bytes, NULL) != APPNP_OK ||
           hipDeviceSynchronize() != hipSuccess)
-        return 4;
+        return -4;
       struct world w;
       memset(&w, 0, sizeof(w));
       pthread_barrier_init(&w.bar, NULL, P);
       pthread_t th[P];
       struct rank_ctx c[P];
       for (int r = 0; r < P; ++r) {
-        c[r] = (struct rank_ctx){&w, r, overlap, drops[di], d_ip, d_ix, nnz, d_H, d_Zref, -1, 0.0};
+        c[r] = (struct rank_ctx){&w,  N,       F,    mode, r,      overlap, drops[di],
+                                 d_ip, d_ix,   nnz,  d_H,  d_Zref, -1,      0.0,      0};
         pthread_create(&th[r], NULL, run_rank, &c[r]);
       }
       for (int r = 0; r < P; ++r) pthread_join(th[r], NULL);
       pthread_barrier_destroy(&w.bar);
       for (int r = 0; r < P; ++r) {
-        const int ok = c[r].rc == APPNP_OK && c[r].err <= 1e-5;
-        printf("rank %d overlap %d p_drop %.2f: rc %d max err %.3e %s\n", r, overlap, drops[di],
-               c[r].rc, c[r].err, ok ? "ok" : "FAIL");
+        /* the split case must take the split layout: one remainder pass per iteration */
+        const int path_ok = sb ? c[r].rem_launches == K : c[r].rem_launches == 0;
+        const int ok = c[r].rc == APPNP_OK && c[r].err <= 1e-5 && path_ok;
+        printf("n %lld F %lld rank %d overlap %d p_drop %.2f: rc %d max err %.3e remainder "
+               "passes %lld %s\n",
+               (long long)N, (long long)F, r, overlap, drops[di], c[r].rc, c[r].err,
+               (long long)c[r].rem_launches, ok ? "ok" : "FAIL");
         failures += !ok;
       }
     }
@@ -183,10 +204,19 @@ int main(void) {
   hipFree(d_H);
   hipFree(d_Zref);
   hipFree(d_ws);
+  free(adj);
+  free(cnt);
   free(indptr);
   free(indices);
   free(H);
-  if (failures) return 5;
+  return failures;
+}
+
+int main(void) {
+  const int a = run_case(3001, 12, 0);
+  const int b = run_case(300001, 100, 1);  /* > 2^16 nodes, few near entries */
+  if (a < 0 || b < 0) return 2;
+  if (a + b) return 5;
   printf("dist_smoke ok\n");
   return 0;
 }
