@@ -251,6 +251,30 @@ def test_bench_two_ranks_autotune_and_parity():
     assert len(tried) >= 2 and all(v is not None for v in tried.values()), tried
 
 
+def test_bench_eight_ranks_every_candidate():
+    """The driver's N = 8 command on the one GPU (eight ranks time-sliced, gloo exchange) on
+    arxiv-synth: every candidate of candidate_layouts(8) -- column, 2x4 and 4x2 with both
+    exchanges, the row partition from Python and from the library's loop -- is measured, the
+    printed line is one of them with parity, the CPU baseline and a coherent roofline
+    (frac <= ceiling.frac <= 1)."""
+    import json
+
+    env = dict(os.environ, PPNP_DIST_BACKEND="gloo", PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=8",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.join(ROOT, "bench.py"), "--gpus", "8", "--workload", "arxiv-synth",
+           "--steps", "2", "--warmup", "1"]
+    proc = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=280)
+    assert proc.returncode == 0, proc.stdout[-3000:] + proc.stderr[-3000:]
+    res = json.loads([l for l in proc.stdout.splitlines() if l.startswith("{")][-1])
+    tried = res["config"]["autotune_ms_per_step"]
+    assert len(tried) == 7 and all(isinstance(v, float) for v in tried.values()), tried
+    assert res["config"]["parallelism"] in tried and res["parity"]["ok"]
+    assert res["cpu_baseline"]["value"] > 0 and res["parity_cpu"]["ok"]
+    rl = res["roofline"]
+    assert 0 < rl["frac"] <= rl["ceiling"]["frac"] <= 1.0
+
+
 @pytest.mark.parametrize("ranks,extra", [
     (2, ["--overlap"]), (2, []), (3, ["--overlap", "--p-drop", "0.3"]),
     (2, ["--dtype", "bf16"]), (4, ["--workload", "arxiv-synth", "--overlap"])])
