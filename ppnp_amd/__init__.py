@@ -8,7 +8,8 @@ model.py:63, as hand-written HIP kernels behind the C ABI in include/ppnp_amd.h.
 from . import _lib
 from .graph import Graph
 from .model import APPNP, PPNP, CustomLinear
-from .ops import propagate, propagate_backward, propagate_forward, step
+from .ops import (propagate, propagate_backward, propagate_forward, split_copy, step,
+                  step_split)
 from .sparse import SparseFeatures, sparse_linear
 
 __all__ = [
@@ -20,6 +21,8 @@ __all__ = [
     "propagate_forward",
     "propagate_backward",
     "step",
+    "step_split",
+    "split_copy",
     "SparseFeatures",
     "sparse_linear",
     "_lib",
