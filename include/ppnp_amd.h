@@ -320,7 +320,11 @@ typedef int (*appnp_allgather_fn)(void* buf, size_t shard_bytes, int rank, int n
 /* indptr/indices/vals/n/nnz/mode: the WHOLE graph's A on this device, as appnp_graph_create.
  * `mode` may carry APPNP_GRAPH_SOURCE_BLOCKS / _SB_W8 / _SB_W16: then fp32 propagations whose
  * F splits (appnp_split_layout) with 16-B aligned H / Z run on the split layout (main part
- * gathers whole lines, remainder pass; appnp_step_split).
+ * gathers whole lines, remainder pass; appnp_step_split).  Every rank must take that path or
+ * none: the rule is the same on every rank (its gather-locality measure is taken over the whole
+ * A), and since the copy is best-effort, the first fp32 propagation with K >= 2 agrees through
+ * one small exchange in the workspace that every rank built it (that call synchronises the
+ * stream once).  H and Z must allow 16-B vectors on every rank alike.
  * overlap != 0 keeps the held rows as local- and remote-column CSRs (fp32 propagation only).
  * allgather/ctx: the exchange, called by every rank once per exchanged iterate (twice on the
  * split layout: its main part, then its remainder part). */

@@ -397,6 +397,25 @@ __global__ __launch_bounds__(kBlock) void k_rb_walk(const int32_t* __restrict__ 
   }
 }
 
+// Off-diagonal entries of A within kNearRows of their row, over ALL n rows (the gather-locality
+// measure of a row-partitioned graph: every rank computes the same value from the same A, so
+// every rank takes the same split decision).  Thread per row, grid-stride.
+__global__ __launch_bounds__(kBlock) void k_near_all(const int32_t* __restrict__ rp,
+                                                     const int32_t* __restrict__ col, int64_t n,
+                                                     unsigned long long* __restrict__ near) {
+  unsigned long long nr = 0;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kBlock) {
+    for (int32_t e = rp[i]; e < rp[i + 1]; ++e) {
+      const int64_t d = (int64_t)col[e] - i;
+      nr += (d != 0 && d < kNearRows && d > -kNearRows) ? 1 : 0;
+    }
+  }
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) nr += __shfl_xor(nr, o);
+  if ((threadIdx.x & (kWave - 1)) == 0 && nr) atomicAdd(near, nr);
+}
+
 // cblk[c] = b for every chunk c of segment (group, block b).  Thread per segment.
 __global__ __launch_bounds__(kBlock) void k_rb_chunks(const int32_t* __restrict__ off,
                                                       int64_t cells, int nb, int chunk,
@@ -490,9 +509,11 @@ int env_or(const char* name, int dflt) {
 // The regrouped copy of A_hat for the persistent remainder pass.  Best-effort at the caller
 // (appnp_graph_create_rows): APPNP_ENOTSUP / APPNP_ERANGE / APPNP_ENOMEM leave the graph
 // without it, and appnp_propagate gathers whole rows.
-int graph_build_source_blocks(appnp_graph* g, int lpe, hipStream_t s) {
+int graph_build_source_blocks(appnp_graph* g, int lpe, const int32_t* a_indptr,
+                              const int32_t* a_indices, int64_t a_nnz, hipStream_t s) {
   // the held rows [row_lo, row_hi) in row groups; source blocks over all n global columns
   const int64_t rows = g->row_hi - g->row_lo;
+  const bool partial = g->row_lo != 0 || rows != g->n;
   if (lpe != 1 && lpe != 2 && lpe != 4) return APPNP_EINVAL;
   const int chunk = kRemChunk / lpe;     // entries per chunk (one per lpe lanes)
   const int max_rg = kRemMaxRg / lpe;    // rows per wave group: 16 x max_rg x 16 lpe B of LDS
@@ -545,6 +566,14 @@ int graph_build_source_blocks(appnp_graph* g, int lpe, hipStream_t s) {
                        nullptr,
                        nullptr,
                        nullptr, reinterpret_cast<unsigned long long*>(tot + 1));
+    if (partial && a_nnz > 0 && ok(hipGetLastError()) &&
+        ok(hipMemsetAsync(tot + 1, 0, sizeof(int64_t), s))) {
+      // the near count of the WHOLE A (replacing the held rows' count of the walk)
+      const int64_t nblk = std::min<int64_t>((g->n + kBlock - 1) / kBlock, 4096);
+      hipLaunchKernelGGL(k_near_all, dim3((unsigned)std::max<int64_t>(1, nblk)), dim3(kBlock), 0,
+                         s, a_indptr, a_indices, g->n,
+                         reinterpret_cast<unsigned long long*>(tot + 1));
+    }
     if (ok(hipGetLastError()) && ok(exclusive_scan(cnt, cells, g->rb_off, bsum, tot, s)) &&
         ok(hipMemcpyAsync(h_tot, tot, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, s)) &&
         ok(hipStreamSynchronize(s))) {
@@ -581,8 +610,11 @@ int graph_build_source_blocks(appnp_graph* g, int lpe, hipStream_t s) {
       if (ok(hipGetLastError()))
         hipLaunchKernelGGL(k_rb_chunks, dim3((unsigned)((cells + kBlock - 1) / kBlock)),
                            dim3(kBlock), 0, s, g->rb_off, cells, (int)nb, chunk, g->rb_cblk);
+      // near entries per entry of A_hat: the held rows' (full graph) or the whole graph's
+      // (row partition: A's off-diagonal entries + the n diagonal ones)
+      const double denom = partial ? (double)(a_nnz + g->n) : (double)g->nnz_hat;
       if (ok(hipGetLastError()) && ok(hipStreamSynchronize(s)))
-        g->near_frac = g->nnz_hat > 0 ? (double)h_tot[1] / (double)g->nnz_hat : 0.0;
+        g->near_frac = denom > 0 ? (double)h_tot[1] / denom : 0.0;
     }
   }
   if (cnt) (void)hipFree(cnt);

@@ -273,7 +273,8 @@ int appnp_graph_create_rows(const int32_t* indptr, const int32_t* indices, const
   // large for the copy (block or segment count, device memory) keeps whole-row gathers --
   // appnp_graph_source_blocks reports whether it was built.
   if (rc == APPNP_OK && want_sb) {
-    const int sb = appnp::graph_build_source_blocks(g, sb_lpe, as_stream(stream));
+    const int sb =
+        appnp::graph_build_source_blocks(g, sb_lpe, indptr, indices, nnz, as_stream(stream));
     if (sb != APPNP_OK && sb != APPNP_ENOTSUP && sb != APPNP_ERANGE && sb != APPNP_ENOMEM)
       rc = sb;
   }

@@ -29,6 +29,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <new>
+#include <vector>
 
 #include "../../include/ppnp_amd.h"
 #include "appnp_internal.h"
@@ -39,6 +40,9 @@ struct appnp_dist {
   int rank = 0, nranks = 1, overlap = 0;
   appnp_allgather_fn allgather = nullptr;
   void* ctx = nullptr;
+  int sb_requested = 0;                // `mode` asked for the source-blocked copy (all ranks)
+  int split_agreed = 0;                // the ranks have agreed on split_ok (first propagation)
+  int split_ok = 0;                    // every rank holds its rows' source-blocked copy
   hipStream_t xs = nullptr;            // exchange stream (overlap)
   hipEvent_t produced = nullptr;       // dst rows written on the caller's stream
   hipEvent_t exchanged = nullptr;      // exchange finished on xs
@@ -85,6 +89,31 @@ WsLayout ws_layout(const appnp_dist* d, int64_t f, int dtype) {
     w.split_total = 2 * w.part_bytes + (d->overlap ? align_up((size_t)d->shard * w.fs * 4) : 0);
   }
   return w;
+}
+
+// The split layout exchanges two parts per iterate, so every rank must take it or none.  The
+// rule is the same on every rank (its locality measure is the whole graph's), but the
+// regrouped copy is best-effort: at the first fp32 propagation with K >= 2 of an engine whose
+// `mode` asked for the copy, the ranks agree through the exchange itself -- each sets one byte
+// of its slot of a small in-place all-gather in the workspace, and the copy is used only if
+// every rank built it.  Synchronises the stream once.
+int agree_split(appnp_dist* d, void* ws, hipStream_t s) {
+  constexpr size_t kSlot = 256;
+  d->split_agreed = 1;
+  d->split_ok = d->g->rb_off != nullptr;
+  if (d->nranks <= 1) return APPNP_OK;
+  char* flags = static_cast<char*>(ws);
+  std::vector<unsigned char> host((size_t)d->nranks, 0);
+  int rc = dev_err(hipMemsetAsync(flags, 0, kSlot * d->nranks, s));
+  if (rc == APPNP_OK && d->split_ok)
+    rc = dev_err(hipMemsetAsync(flags + kSlot * d->rank, 1, 1, s));
+  if (rc == APPNP_OK) rc = d->allgather(flags, kSlot, d->rank, d->nranks, s, d->ctx);
+  for (int p = 0; p < d->nranks && rc == APPNP_OK; ++p)
+    rc = dev_err(hipMemcpyAsync(&host[p], flags + kSlot * p, 1, hipMemcpyDeviceToHost, s));
+  if (rc == APPNP_OK) rc = dev_err(hipStreamSynchronize(s));
+  for (int p = 0; p < d->nranks; ++p)
+    if (rc != APPNP_OK || host[p] != 1) d->split_ok = 0;
+  return rc;
 }
 
 bool aligned16(const void* p, int64_t ld) {
@@ -202,6 +231,8 @@ int appnp_dist_create(const int32_t* indptr, const int32_t* indices, const float
   d->hi = std::min<int64_t>(n, d->lo + d->shard);
   int rc = appnp_graph_create_rows(indptr, indices, vals, n, nnz, mode, d->lo, d->hi,
                                    d->overlap, stream, &d->g);
+  d->sb_requested = (mode & (APPNP_GRAPH_SOURCE_BLOCKS | APPNP_GRAPH_SB_W8 |
+                             APPNP_GRAPH_SB_W16)) != 0;
   if (rc == APPNP_OK && d->overlap) {
     rc = dev_err(hipStreamCreateWithFlags(&d->xs, hipStreamNonBlocking));
     if (rc == APPNP_OK) rc = dev_err(hipEventCreateWithFlags(&d->produced, hipEventDisableTiming));
@@ -246,9 +277,17 @@ int appnp_dist_propagate(appnp_dist* d, const void* H, int64_t ld_h, void* Z, in
   hipStream_t s = as_stream(stream);
   if (K == 0) return dev_err(copy_rows(Z, ld_z, H, ld_h, rows, f, es, s));
   const WsLayout w = ws_layout(d, f, dtype);
-  // split rows when the held rows' copy allows it and H / Z allow 16-B vectors (K >= 2: one
-  // iteration gains nothing from the split layout)
-  if (w.split_total && K >= 2 && (rows == 0 || (aligned16(H, ld_h) && aligned16(Z, ld_z)))) {
+  if (d->sb_requested && !d->split_agreed && dtype == APPNP_F32 && K >= 2) {
+    if (!ws || ws_bytes < w.total || ws_bytes < 256 * (size_t)d->nranks) return APPNP_EINVAL;
+    const int arc = agree_split(d, ws, s);
+    if (arc != APPNP_OK) return arc;
+  }
+  // split rows when every rank's copy allows it and H / Z allow 16-B vectors (K >= 2: one
+  // iteration gains nothing from the split layout).  Collective: H and Z must allow 16-B
+  // vectors on every rank alike, as they do when every rank runs the same code
+  // (include/ppnp_amd.h)
+  if (d->split_ok && w.split_total && K >= 2 &&
+      (rows == 0 || (aligned16(H, ld_h) && aligned16(Z, ld_z)))) {
     if (!ws || ws_bytes < w.split_total) return APPNP_EINVAL;
     return propagate_split_rows(d, w, static_cast<const float*>(H), ld_h, static_cast<float*>(Z),
                                 ld_z, f, K, alpha, p_drop, seed, static_cast<char*>(ws), s);

@@ -88,7 +88,10 @@ hipError_t exclusive_scan(const int32_t* cnt, int64_t rows, int32_t* out, int64_
 
 // appnp_blocks.hip
 // lpe: lanes per entry of the remainder pass (1, 2, 4: remainder rows of 4, 8, 16 columns)
-int graph_build_source_blocks(appnp_graph* g, int lpe, hipStream_t s);
+// a_indptr / a_indices / a_nnz: the whole graph's A (the row partition's gather-locality
+// measure is taken over all of it, so every rank decides the same split)
+int graph_build_source_blocks(appnp_graph* g, int lpe, const int32_t* a_indptr,
+                              const int32_t* a_indices, int64_t a_nnz, hipStream_t s);
 // to_rem: out is the next remainder buffer (a unit graph stores dr o y there), not Z / dH
 hipError_t launch_remainder(const appnp_graph* g, const StepArgs& a, int epi,
                             const float* z_rem, const float* h_rem, int64_t ld_h, float* out,

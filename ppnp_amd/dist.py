@@ -399,6 +399,16 @@ class PartitionedAPPNP:
         if (layout.rows > 1 and step_fn is None and K >= 2 and H.dtype == torch.float32
                 and ld % 4 == 0 and hasattr(graph, "split_layout")):
             split = graph.split_layout(width)
+            # every rank must take the same path (the split exchanges two parts per iterate):
+            # the rule itself is the same everywhere (the locality measure is the whole
+            # graph's), but the regrouped copy is best-effort, so agree over the ranks
+            if dist.is_initialized() and layout.rows > 1:
+                on_gpu = dist.get_backend() == "nccl"
+                t = torch.tensor([1 if split else 0], dtype=torch.int32,
+                                 device=device if on_gpu else "cpu")
+                dist.all_reduce(t, op=dist.ReduceOp.MIN)
+                if not int(t.item()):
+                    split = None
         if split is None:
             bufs = [torch.zeros(rows_pad, ld, dtype=H.dtype, device=device) for _ in range(2)]
             partial = (torch.zeros(max(hi - lo, 0), ld, dtype=torch.float32, device=device)

@@ -34,6 +34,9 @@ def main():
     p.add_argument("--split", action="store_true",
                    help="build the held rows' source-blocked copy for F (split rows) and fail "
                         "unless the engine takes the split layout")
+    p.add_argument("--sb-oom-rank", type=int, default=-1,
+                   help="this rank's copy fails to build (APPNP_SB_TEST_OOM): the engines must "
+                        "agree on whole rows everywhere")
     a = p.parse_args()
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
@@ -55,6 +58,8 @@ def main():
     indptr, indices = synth.graph_for(a.workload, device=dev)
     H = synth.features(n, F, dtype=dtype, device=dev, seed=1)
 
+    if rank == a.sb_oom_rank:
+        os.environ["APPNP_SB_TEST_OOM"] = "1"
     runner = pdist.NativeRowAPPNP(indptr, indices, n, dev, overlap=a.overlap,
                                   features=F if a.split else None, dtype=dtype)
     g = pdist._DistGraphInfo(C.c_void_p(_lib.load().appnp_dist_graph(runner._h)))
@@ -71,7 +76,8 @@ def main():
     err = (Z.double() - block.double()).abs().max().item() if block.numel() else 0.0
     scale = ref.abs().max().item()
     tol = (1e-5 if dtype == torch.float32 else 1e-2) * scale + 1e-6
-    ok = err <= tol and (split_ran == a.split or runner.hi == runner.lo)
+    want_split = a.split and a.sb_oom_rank < 0
+    ok = err <= tol and (split_ran == want_split or runner.hi == runner.lo)
     extra = f" split={split_ran}"
     if backend == "nccl" and world == 1:
         # the library's RCCL callback on torch's communicator: a one-rank in-place all-gather

@@ -43,6 +43,9 @@ def main():
                         "the single-GPU HIP propagation")
     p.add_argument("--expect-split", type=int, default=None,
                    help="fail unless the rank's remainder columns (split rows) equal this")
+    p.add_argument("--sb-oom-rank", type=int, default=-1,
+                   help="this rank's source-blocked copy fails to build (APPNP_SB_TEST_OOM): "
+                        "every rank must then keep whole rows")
     a = p.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -66,6 +69,8 @@ def main():
     else:
         indptr, indices = synth.uniform_graph(a.n, a.m, 7, device=dev)
     H = synth.features(a.n, a.f, device=dev, seed=1)
+    if rank == a.sb_oom_rank:
+        os.environ["APPNP_SB_TEST_OOM"] = "1"
     runner = pdist.PartitionedAPPNP.create(indptr, indices, a.n, H, a.K, a.alpha, dev,
                                            layout=layout, overlap=a.overlap,
                                            p_drop=a.p_drop, seed=5, exchange=a.exchange)

@@ -338,6 +338,29 @@ def test_row_partition_split_rows_matches_oracle(ranks, extra):
     assert res == {r: "OK" for r in range(ranks)}, proc.stdout[-4000:]
 
 
+def test_split_decision_is_collective():
+    """The regrouped copy is best-effort: when it cannot be built on ONE rank (rank 1 here,
+    APPNP_SB_TEST_OOM), every rank keeps whole rows -- both the Python row loop (an all-reduce at
+    create) and the library's engine (one small exchange at the first propagation) -- instead
+    of exchanging two parts on some ranks and one on others.  Results still match."""
+    env = dict(os.environ, PPNP_DIST_BACKEND="gloo", PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
+    base = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+            "--master-addr=127.0.0.1"]
+    py = base + [f"--master-port={_free_port()}", os.path.join(ROOT, "tests", "dist_worker.py"),
+                 "--layout", "row", "--graph-n", "200000", "--graph-m", "1000000", "--f", "100",
+                 "--K", "3", "--expect-split", "0", "--sb-oom-rank", "1", "--overlap"]
+    proc = subprocess.run(py, env=env, cwd=ROOT, capture_output=True, text=True, timeout=150)
+    assert proc.returncode == 0, proc.stdout[-3000:] + proc.stderr[-3000:]
+    assert _rank_results(proc.stdout, "dist_worker") == {0: "OK", 1: "OK"}, proc.stdout[-4000:]
+    nat = base + [f"--master-port={_free_port()}",
+                  os.path.join(ROOT, "tests", "dist_capi_worker.py"), "--workload", "arxiv-synth",
+                  "--features", "100", "--split", "--sb-oom-rank", "1", "--overlap"]
+    proc = subprocess.run(nat, env=env, cwd=ROOT, capture_output=True, text=True, timeout=150)
+    assert proc.returncode == 0, proc.stdout[-3000:] + proc.stderr[-3000:]
+    assert _rank_results(proc.stdout, "dist_capi") == {0: "OK", 1: "OK"}, proc.stdout[-4000:]
+    assert proc.stdout.count("split=False") == 2, proc.stdout[-4000:]
+
+
 @pytest.mark.parametrize("ranks,extra", [(2, []), (2, ["--overlap", "--p-drop", "0.3"]),
                                          (3, ["--overlap"])])
 def test_native_row_engine_split_rows(ranks, extra):
