@@ -396,13 +396,16 @@ class PartitionedAPPNP:
         H_slab = torch.zeros(max(hi - lo, 0), ld, dtype=H.dtype, device=device)
         H_slab[:, :width] = H[lo:hi, f_lo:f_hi].to(device)
         split = None
-        if (layout.rows > 1 and step_fn is None and K >= 2 and H.dtype == torch.float32
-                and ld % 4 == 0 and hasattr(graph, "split_layout")):
-            split = graph.split_layout(width)
-            # every rank must take the same path (the split exchanges two parts per iterate):
-            # the rule itself is the same everywhere (the locality measure is the whole
-            # graph's), but the regrouped copy is best-effort, so agree over the ranks
-            if dist.is_initialized() and layout.rows > 1:
+        if layout.rows > 1 and step_fn is None:
+            if (K >= 2 and H.dtype == torch.float32 and ld % 4 == 0
+                    and hasattr(graph, "split_layout")):
+                split = graph.split_layout(width)
+            # every rank must take the same path (the split exchanges two parts per iterate,
+            # and the relayed exchange spans all ranks): the rule is the same everywhere (the
+            # locality measure is the whole graph's), but slab widths can differ between column
+            # groups and the regrouped copy is best-effort, so all ranks agree -- every rank
+            # takes part, whatever it found
+            if dist.is_initialized() and layout.size > 1:
                 on_gpu = dist.get_backend() == "nccl"
                 t = torch.tensor([1 if split else 0], dtype=torch.int32,
                                  device=device if on_gpu else "cpu")
