@@ -2,7 +2,7 @@
 // (k_rem_persist, 16-B rows) widened to W = 4 * LPE fp32 columns.  Not part of the library.
 //
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 tools/blk_probe.hip -o tools/bin/blk_probe
-//   [BLK_N=n BLK_DEG=d] tools/bin/blk_probe W:br:U [W:br:U ...]   (W in 4, 8, 16, 32; br = log2 source rows
+//   [BLK_N=n BLK_DEG=d] tools/bin/blk_probe W:br:U[:em] [...]   (W in 4, 8, 16, 32; br = log2 source rows
 //                                                 per block; U = chunks in flight per wave)
 //
 // Question: the random-gather SpMM is bound by ~56 G line requests/s from
@@ -177,6 +177,79 @@ __global__ __launch_bounds__(kThreads) void k_blk(const int* __restrict__ off,
   }
 }
 
+// Entry-major variant: lane = e * LPE + q, so the LPE lanes of one entry read its row's
+// W * 4 contiguous bytes in one go (one L1 tag lookup / L2 request instead of LPE); the
+// gathered pieces (and entry words) are then moved to the quarter-major order of k_blk by
+// ds_bpermute, and the scan and LDS update are k_blk's.
+template <int LPE, int U>
+__global__ __launch_bounds__(kThreads) void k_blk_em(const int* __restrict__ off,
+                                                     const uint32_t* __restrict__ ent,
+                                                     const int* __restrict__ cblk, int br_log2,
+                                                     int nb, int slots, int rg, int passes,
+                                                     float w, const f4* __restrict__ z,
+                                                     f4* __restrict__ y, int n) {
+  constexpr int CH = 64 / LPE;
+  extern __shared__ f4 acc_all[];
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int q = lane / CH, e = lane % CH;          // quarter-major position (scan, LDS)
+  const int le = lane / LPE, lq = lane % LPE;      // entry-major position (gather)
+  const int src = (e * LPE + q) * 4;               // bpermute byte address of my piece
+  f4* acc = acc_all + (int64_t)wv * rg * LPE;
+  const uint32_t cmask = (1u << kColBits) - 1u;
+  unsigned long long first = 0;
+  for (int t = 0; t < LPE; ++t) first |= 1ull << (t * CH);
+  for (int p = 0; p < passes; ++p) {
+    const int64_t g = (int64_t)p * slots + (int64_t)blockIdx.x * kWaves + wv;
+    const int64_t r0 = g * rg;
+    const int64_t left = n - r0;
+    const int rows = left <= 0 ? 0 : (left < rg ? (int)left : rg);
+    for (int i = lane; i < rows * LPE; i += 64) acc[i] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+    const int c_end = off[(g + 1) * nb] / CH;
+    for (int c = off[g * nb] / CH; c < c_end; c += U) {
+      const int nch = c_end - c < U ? c_end - c : U;
+      uint32_t en[U];
+      int cb[U];
+      f4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        en[u] = kNone;
+        cb[u] = 0;
+        if (u < nch) {
+          en[u] = __builtin_nontemporal_load(ent + (int64_t)(c + u) * CH + le);
+          cb[u] = cblk[c + u] << br_log2;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        v[u] = en[u] != kNone ? z[(int64_t)(cb[u] + (int)(en[u] & cmask)) * LPE + lq]
+                              : f4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (u >= nch) break;
+        const uint32_t ew = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)en[u]);
+        f4 s;
+        s.x = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(v[u].x)));
+        s.y = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(v[u].y)));
+        s.z = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(v[u].z)));
+        s.w = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(v[u].w)));
+        const bool act = ew != kNone;
+        const int row = (int)(ew >> kColBits);
+        const int key = (row << 3) | q;
+        const int prev = __builtin_amdgcn_update_dpp(-1, key, 0x138, 0xf, 0xf, false);
+        const unsigned long long heads = __ballot(prev != key || !act) | first;
+        seg_scan<CH>(key, s, heads);
+        const bool tail = e == CH - 1 || ((heads >> (lane + 1)) & 1ull);
+        if (act && tail) {
+          const f4 a = acc[row * LPE + q];
+          acc[row * LPE + q] = a + s;
+        }
+      }
+    }
+    for (int i = lane; i < rows * LPE; i += 64) y[r0 * LPE + i] = acc[i] * w;
+  }
+}
+
 struct Graph {
   int n;
   int64_t nnz;
@@ -201,7 +274,7 @@ float run_direct(const Graph& G, const int* d_rp, const int* d_col, const f4* d_
   return ms / 10;
 }
 
-template <int LPE, int U>
+template <int LPE, int U, bool EM>
 float run_blk(const Graph& G, int br, const f4* d_z, f4* d_y, float w, hipEvent_t a,
               hipEvent_t b, double* pad, int cus) {
   constexpr int CH = 64 / LPE;
@@ -244,11 +317,12 @@ float run_blk(const Graph& G, int br, const f4* d_z, f4* d_y, float w, hipEvent_
   CHECK(hipMemcpy(d_off, off.data(), off.size() * 4, hipMemcpyHostToDevice));
   CHECK(hipMemcpy(d_ent, ent.data(), tot * 4, hipMemcpyHostToDevice));
   CHECK(hipMemcpy(d_cblk, cblk.data(), cblk.size() * 4, hipMemcpyHostToDevice));
-  CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_blk<LPE, U>),
+  auto kern = EM ? k_blk_em<LPE, U> : k_blk<LPE, U>;
+  CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                             hipFuncAttributeMaxDynamicSharedMemorySize, kLds));
   const size_t lds = (size_t)kWaves * rg * LPE * 16;
   auto body = [&] {
-    hipLaunchKernelGGL((k_blk<LPE, U>), dim3(cus), dim3(kThreads), lds, 0, d_off, d_ent, d_cblk,
+    hipLaunchKernelGGL(kern, dim3(cus), dim3(kThreads), lds, 0, d_off, d_ent, d_cblk,
                        br, nb, slots, rg, passes, w, d_z, d_y, n);
   };
   for (int i = 0; i < 2; ++i) body();
@@ -315,8 +389,8 @@ int main(int argc, char** argv) {
   printf("variant      W  block_rows  U  ms_per_pass  G_nonzeros_per_s  padding  max|diff|\n");
   std::vector<float> y0, y1;
   for (int ai = 1; ai < argc; ++ai) {
-    int W = 16, br = 14, U = 2;
-    if (sscanf(argv[ai], "%d:%d:%d", &W, &br, &U) < 1) continue;
+    int W = 16, br = 14, U = 2, em = 0;
+    if (sscanf(argv[ai], "%d:%d:%d:%d", &W, &br, &U, &em) < 1) continue;
     const size_t ny = (size_t)n * W;
     y0.assign(ny, 0.0f);
     y1.assign(ny, 0.0f);
@@ -336,7 +410,8 @@ int main(int argc, char** argv) {
     CHECK(hipMemset(d_y1, 0, ny * 4));
     double pad = 0.0;
     float t = 0.0f;
-#define BLK(L, UU) t = run_blk<L, UU>(G, br, d_z, d_y1, w, a, b, &pad, cus)
+#define BLK(L, UU) t = em ? run_blk<L, UU, true>(G, br, d_z, d_y1, w, a, b, &pad, cus) \
+                            : run_blk<L, UU, false>(G, br, d_z, d_y1, w, a, b, &pad, cus)
     if (W == 4) { if (U == 1) BLK(1, 1); else if (U == 2) BLK(1, 2); else BLK(1, 4); }
     if (W == 8) { if (U == 1) BLK(2, 1); else if (U == 2) BLK(2, 2); else BLK(2, 4); }
     if (W == 16) { if (U == 1) BLK(4, 1); else if (U == 2) BLK(4, 2); else BLK(4, 4); }
@@ -348,8 +423,8 @@ int main(int argc, char** argv) {
       err = std::max(err, (double)std::fabs(y0[i] - y1[i]));
       mx = std::max(mx, (double)std::fabs(y0[i]));
     }
-    printf("blocked    %3d  %10d  %d  %11.3f  %16.1f  %6.1f %%  %.2e of %.2e\n", W, 1 << br, U,
-           t, G.nnz / (t * 1e6), 100.0 * pad, err, mx);
+    printf("%s %3d  %10d  %d  %11.3f  %16.1f  %6.1f %%  %.2e of %.2e\n",
+           em ? "blocked-em" : "blocked   ", W, 1 << br, U, t, G.nnz / (t * 1e6), 100.0 * pad, err, mx);
     fflush(stdout);
   }
   return 0;
