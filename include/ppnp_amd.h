@@ -74,9 +74,11 @@ enum appnp_norm { APPNP_NORM_SYM = 0, APPNP_NORM_RW = 1 };
 
 /* OR into `mode` instead of (or with) APPNP_GRAPH_SOURCE_BLOCKS: the source-blocked copy for a
  * remainder of up to 8 (W8) or 16 (W16) columns: fp32 rows of F = 32q + r features with
- * r <= 8 (a wider remainder beside a main part costs as much as its extra line, measured), and
- * narrow rows F <= 8 / 16 whole (for example F = 40 = 32 + 8, or the 12-13-column slabs of an
- * 8-rank column layout of F = 100).  The pass then gives 2 / 4 lanes to each
+ * r <= 8 on a W8 copy (a wider remainder beside a main part costs as much as its extra line,
+ * measured), and narrow rows F <= 8 / 16 whole (for example F = 40 = 32 + 8, or the 12-13-column
+ * slabs of an 8-rank column layout of F = 100).  A W16 copy serves narrow rows only: beside a
+ * main part its 4 row passes cost more than the extra line (F = 100 / 36 measured), so such
+ * rows stay whole on it.  The pass then gives 2 / 4 lanes to each
  * entry and holds 320 / 160 rows per wave group, so a graph may need 2 / 4 row passes per
  * launch.  Same memory as APPNP_GRAPH_SOURCE_BLOCKS (segments padded to 32 / 16 entries). */
 #define APPNP_GRAPH_SB_W8 0x400
@@ -184,14 +186,15 @@ size_t appnp_workspace_bytes(const appnp_graph* g, int64_t f, int64_t ld, int dt
  * leading dimensions that are multiples of 4 floats (K >= 2): columns [0, *fs) gather whole cache
  * lines and [*fs, F) run the persistent L2-blocked remainder pass.  fp32 rows of F = 32q + r
  * features take it on a graph built with a source-blocked copy, above 2^16 nodes and without
- * gather locality: r <= 4 on an APPNP_GRAPH_SOURCE_BLOCKS copy, r <= 8 on an APPNP_GRAPH_SB_W8 /
- * _W16 copy (wider remainders beside a main part keep whole rows).  *fs = 0 when rows are
+ * gather locality: r <= 4 on an APPNP_GRAPH_SOURCE_BLOCKS copy, r <= 8 on an APPNP_GRAPH_SB_W8
+ * copy (wider remainders beside a main part keep whole rows, and so does every F > 32 on an
+ * APPNP_GRAPH_SB_W16 copy).  *fs = 0 when rows are
  * gathered whole, and also for narrow rows, which run wholly in the pass (see below).
  * Informational: appnp_propagate decides by itself, on the same rule. */
 int appnp_propagate_split_point(const appnp_graph* g, int64_t f, int dtype, int64_t* fs);
 
 /* The remainder columns of that split: *r = F - fs columns run the L2-blocked pass -- 1-4 on an
- * APPNP_GRAPH_SOURCE_BLOCKS copy, up to 8 on a W8 / W16 copy -- and narrow rows F <= 4 / 8 / 16
+ * APPNP_GRAPH_SOURCE_BLOCKS copy, up to 8 on a W8 copy -- and narrow rows F <= 4 / 8 / 16
  * (the copy's width) run wholly in the pass, *r = F with *fs = 0.  *r = 0 when rows are
  * gathered whole. */
 int appnp_propagate_remainder_cols(const appnp_graph* g, int64_t f, int dtype, int64_t* r);

@@ -95,8 +95,8 @@ bool vec16(const int64_t* lds, int n_ld, const void* const* ptrs, int n_ptr) {
 // Split rows (appnp_blocks.hip): the remainder columns r of fp32 rows of F = 32q + r features run
 // as a separate chain of persistent L2-resident passes over the source-blocked A_hat, and the
 // main part f - r (a multiple of 32, possibly 0) gathers whole lines from the split layout
-// [n, 32q].  r <= 4 rb_lpe: 1-4 columns on a graph built with APPNP_GRAPH_SOURCE_BLOCKS, up to
-// 8 / 16 with APPNP_GRAPH_SB_W8 / _W16; narrow rows (f <= 4 rb_lpe) run wholly in the pass.
+// [n, 32q].  1-4 columns on a graph built with APPNP_GRAPH_SOURCE_BLOCKS, up to 8 with
+// APPNP_GRAPH_SB_W8; narrow rows (f <= 4 rb_lpe: 4 / 8 / 16 with _W16) run wholly in the pass.
 // Returns 0 (rows gathered whole) when the path does not apply: no blocked copy, bf16,
 // latency-regime graph, F outside [1, 256], operands that do not allow 16-B vectors
 // (``aligned``), or a graph with gather locality.  APPNP_SPLIT=0 disables it (measurement).
@@ -115,6 +115,11 @@ int64_t remainder_cols(const appnp_graph* g, int64_t f, int dtype, bool aligned)
   // (products-synth F = 47: 4.53 ms split against 4.41 ms whole rows; F = 40 = 32 + 8: 3.68
   // against 4.44 ms; profiles/r2_wide_remainder.txt)
   if (f > 32 && r > 8) return 0;
+  // and beside a main part, the 4-lane pass of a W16 copy (4 row passes) costs more than the
+  // extra line even for r <= 4 (products-synth F = 100: 9.44 ms split on W16 against 9.20 whole
+  // rows and 7.77 on W4; F = 36: 4.50 against 4.42; profiles/r3_wide_copy_f100.txt).
+  // A W8 copy still wins there (F = 100: 8.21 ms), so only W16 keeps whole rows
+  if (f > 32 && g->rb_lpe == 4) return 0;
   return (r >= 1 && r <= w) ? r : 0;
 }
 

@@ -314,13 +314,15 @@ def wide(adj):
                                  (16, 100)])
 @pytest.mark.parametrize("K", [2, 3])
 def test_wide_remainder_matches_oracle(wide, ahat, w, f, K):
-    """Remainders of 5-8 columns and narrow rows against the float64 oracle (F = 100 on these
-    graphs: r = 4 runs the wide pass too; 47, 44, 48 = 32 + 9..16 keep whole rows)."""
+    """Remainders of 5-8 columns and narrow rows against the float64 oracle (F = 100 on the W8
+    graph: r = 4 runs the wide pass too; 47, 44, 48 = 32 + 9..16 keep whole rows, and so does
+    every F > 32 on the W16 graph, whose 4-lane pass costs more than the extra line:
+    profiles/r3_wide_copy_f100.txt)."""
     import ppnp_amd
 
     G = wide[w]
     r = f % 32 if f > 32 else f
-    if f > 32 and r > 8:
+    if f > 32 and (r > 8 or w == 16):
         r = 0
     assert G.remainder_cols(f) == r and G.split_point(f) == (f - r if r else 0)
     H = _h(f, 40 + f + K)
@@ -342,7 +344,8 @@ def test_wide_remainder_limits(wide, graphs):
     """What each layout takes: 17-32 columns and remainders wider than the layout stay whole."""
     assert wide[8].remainder_cols(41) == 0 and wide[8].remainder_cols(12) == 0
     assert wide[16].remainder_cols(20) == 0 and wide[16].remainder_cols(49) == 0
-    assert wide[16].remainder_cols(47) == 0 and wide[16].remainder_cols(40) == 8
+    assert wide[16].remainder_cols(47) == 0 and wide[16].remainder_cols(40) == 0
+    assert wide[16].remainder_cols(100) == 0 and wide[8].remainder_cols(100) == 4
     assert wide[16].remainder_cols(64) == 0 and wide[8].remainder_cols(64) == 0
     assert graphs[0].remainder_cols(3) == 3 and graphs[0].remainder_cols(5) == 0  # W4: narrow <= 4
     assert graphs[1].remainder_cols(3) == 0  # no copy
