@@ -59,6 +59,9 @@ XGMI_IN_GBS = 7 * 76.8
 # L2 read bandwidth, all XCDs (MI355X_MICROARCH.md "L2 (per XCD)": ~34.5 TB/s): bounds the
 # remainder pass, whose gathers are L2 requests
 L2_PEAK_GBS = 34500.0
+# N > 1: nonzero-feature products of the CPU leg's sample (one products-synth iteration is
+# 1.24e10: a sample of 1; arxiv-synth's 3.0e8 per iteration keeps all K = 10)
+CPU_LEG_WORK = 2.0e10
 
 
 def parse(argv=None):
@@ -108,12 +111,16 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def cpu_threads() -> tuple[int, int]:
+def cpu_threads(world: int = 1) -> tuple[int, int]:
     """(threads to use, CPUs this process may run on).  BASELINE.md asks for every core; on the
     GPU box the process's share is what OMP_NUM_THREADS names (16 of a much larger machine, whose
-    full count os.cpu_count() reports), so that bounds it."""
+    full count os.cpu_count() reports), so that bounds it.  At N > 1 torch.distributed.run sets
+    OMP_NUM_THREADS=1 for every rank unless the caller set it; rank 0 runs the CPU leg while the
+    other ranks wait at a barrier, so it takes up to 16 of its visible CPUs regardless."""
     visible = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
     share = int(os.environ.get("OMP_NUM_THREADS") or 0) or visible
+    if world > 1:
+        share = max(share, min(16, visible))
     return max(1, min(visible, share)), visible
 
 
@@ -142,14 +149,14 @@ def committed_traffic(key):
         return None
 
 
-def cpu_baseline(graph, H, K, alpha, iters, adj=None):
+def cpu_baseline(graph, H, K, alpha, iters, adj=None, world=1):
     """Time the oracle's CPU torch.sparse.mm APPNP loop on the same operator and H (SURVEY.md
     8(d) CPU baseline (i)); return (the JSON object, Z of the CPU loop).  For N <= 20k also time
     the reference's as-shipped PPNP path, compute_ppr + dense Pi @ H (helpers.py:68-71,
     model.py:63; baseline (ii))."""
     from oracle import ppnp_oracle as O
 
-    threads, visible = cpu_threads()
+    threads, visible = cpu_threads(world)
     torch.set_num_threads(threads)
     rp, col, val, _ = graph.csr()
     a_t = torch.sparse_csr_tensor(rp.cpu().long(), col.cpu().long(), val.cpu(),
@@ -557,6 +564,11 @@ def main(argv=None):
             f"default_rng) and H generated in {t_gen:.2f}s")
 
     cpu_iters = K if args.cpu_iters is None else args.cpu_iters
+    if args.cpu_iters is None and world > 1:
+        # N > 1: the CPU leg runs once on rank 0 while every other rank waits, and the parity
+        # reference there is the single-GPU propagation, so a large graph gets a bounded sample
+        # (products-synth: 1 of K iterations, ~1 s at 16 threads); small graphs keep all K
+        cpu_iters = max(1, min(K, int(CPU_LEG_WORK // max(1, m * 2 * F))))
     adj_small = None
     if n <= 20000 and rank == 0:  # the as-shipped PPNP leg of the CPU baseline needs A
         import numpy as np
@@ -573,7 +585,7 @@ def main(argv=None):
         the whole graph against its all-K-iterations Z_K."""
         if rank != 0 or cpu_iters <= 0 or args.emulate:
             return
-        cb, Zc = cpu_baseline(graph, H, K, alpha, cpu_iters, adj_small)
+        cb, Zc = cpu_baseline(graph, H, K, alpha, cpu_iters, adj_small, world)
         extras["cpu_baseline"] = cb
         if cpu_iters == K and Zgpu is not None:
             err = float((Zgpu.float().cpu() - Zc).abs().max())

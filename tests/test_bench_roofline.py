@@ -91,3 +91,27 @@ def test_traffic_key_tracks_kernels_and_sources():
     k2 = bench.traffic_key("products-synth", "f32", "single", "k_step[0,96)+k_rem_persist<W4>")
     assert k1 != k2 and k1.startswith("products-synth:f32:single:k_step:src=")
     assert bench.committed_traffic("no-such-key") is None
+
+
+def test_cpu_leg_threads_and_sample(monkeypatch):
+    """N > 1: torch.distributed.run sets OMP_NUM_THREADS=1 per rank, but rank 0 runs the CPU leg
+    while the others wait, so it takes up to 16 visible CPUs; N = 1 keeps the box's share.  The
+    N > 1 sample is bounded: 1 products-synth iteration, all K = 10 of arxiv-synth."""
+    monkeypatch.setattr(bench.os, "sched_getaffinity", lambda pid: set(range(64)), raising=False)
+    monkeypatch.setenv("OMP_NUM_THREADS", "1")
+    assert bench.cpu_threads(1) == (1, 64)
+    assert bench.cpu_threads(8) == (16, 64)
+    monkeypatch.setenv("OMP_NUM_THREADS", "32")
+    assert bench.cpu_threads(8) == (32, 64)
+    monkeypatch.setattr(bench.os, "sched_getaffinity", lambda pid: set(range(4)), raising=False)
+    assert bench.cpu_threads(8) == (4, 4)
+    for workload, iters in (("products-synth", 1), ("arxiv-synth", 10)):
+        n, m, f, k = bench_config(workload)
+        assert max(1, min(k, int(bench.CPU_LEG_WORK // (m * 2 * f)))) == iters
+
+
+def bench_config(workload):
+    from ppnp_amd import synth
+
+    n, m, f, k = synth.CONFIGS[workload][:4]
+    return n, m, f, k
