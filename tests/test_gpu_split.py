@@ -473,3 +473,29 @@ def test_workspace_covers_the_wide_split_layout(wide):
                                  C.c_void_p(torch.cuda.current_stream().cuda_stream))
         assert rc == 0
         assert G.source_block_layout()["launches"] - before == 2, (w, f)
+
+
+@pytest.mark.parametrize("f,ld", [(100, 128), (36, 64), (132, 160), (100, 104)])
+@pytest.mark.parametrize("p", [0.0, 0.25])
+def test_split_from_line_aligned_h(graphs, ahat, f, ld, p):
+    """H in a wider buffer whose padding holds NaN (ld a multiple of 32 floats, whole-line rows,
+    or 104: 16-B but not line aligned), forward and adjoint on the split path against the
+    float64 oracle and bitwise against a packed H: the split copy reads the remainder's last
+    16-B piece across the row end and must zero what lies past column F."""
+    import ppnp_amd
+
+    G = graphs[0]
+    H = _h(f, 90 + f)
+    Hb = torch.full((N, ld), float("nan"), device=DEV)
+    Hb[:, :f] = H.to(DEV)
+    assert Hb.data_ptr() % 128 == 0
+    before = G.source_block_layout()["launches"]
+    Z = ppnp_amd.propagate_forward(G, Hb[:, :f], 3, 0.1, p_drop=p, seed=5)
+    assert G.source_block_layout()["launches"] - before == 3  # the split path
+    close_fp32(Z.double().cpu().numpy(),
+               O.appnp_propagate(ahat, H.numpy(), 3, 0.1, p_drop=p, seed=5))
+    Zp = ppnp_amd.propagate_forward(G, H.to(DEV).contiguous(), 3, 0.1, p_drop=p, seed=5)
+    assert torch.equal(Z, Zp)  # same sums, whichever buffer the first step gathered from
+    dH = ppnp_amd.propagate_backward(G, Hb[:, :f], 3, 0.1, p_drop=p, seed=5)
+    close_fp32(dH.double().cpu().numpy(),
+               O.appnp_backward(ahat, H.numpy(), 3, 0.1, p_drop=p, seed=5))
