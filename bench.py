@@ -431,8 +431,19 @@ def run_candidates(cands, measure, ctl, timeout_s, emit, name_of, rank, world,
                 err = f"{type(e).__name__}: {e}"
             failed = torch.tensor([1.0 if err else 0.0], dtype=torch.float64)
             if world > 1:
-                torch.distributed.all_reduce(failed, op=torch.distributed.ReduceOp.MAX,
-                                             group=ctl)
+                try:
+                    torch.distributed.all_reduce(failed, op=torch.distributed.ReduceOp.MAX,
+                                                 group=ctl)
+                except Exception as e:  # noqa: BLE001
+                    # a peer is gone -- its deadline ended it while this rank had already
+                    # failed or finished the candidate: end the same way, with the best line
+                    log(f"[bench] candidate {name}: agreement failed on rank {rank} "
+                        f"({type(e).__name__}: {e}); a peer has ended")
+                    if guard:
+                        guard._fire()  # unless finish() won the lock, this never returns
+                    else:
+                        expire()
+                    raise
         finally:
             if guard:
                 guard.__exit__(None, None, None)

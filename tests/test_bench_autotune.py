@@ -40,6 +40,12 @@ def _worker(rank, world, port, plan, out, timeout_s):
 
     def measure(tag):
         delay, who, what = plan[tag]
+        if isinstance(who, dict):  # a per-rank action
+            what = who.get(rank)
+            who = rank if what else None
+        if who == rank and what == "die":  # a peer whose own deadline ended it early
+            time.sleep(1.0)
+            os._exit(0)
         mine = who in (rank, "all")
         if mine and what == "raise":
             raise RuntimeError(f"injected exchange failure in {tag}")
@@ -118,6 +124,20 @@ def test_stalled_exchange_still_prints_the_column_line(tmp_path):
     times = line["config"]["autotune_ms_per_step"]
     assert times["2x4-multipath"] == "timeout" and times["col"] >= 20.0
     assert "never" not in times
+
+
+def test_peer_gone_during_agreement_still_prints_the_line(tmp_path):
+    """Rank 0 fails a candidate and waits in the control group's agreement while rank 1 (stuck
+    in the exchange rank 0 never joined) is ended by its own deadline first: rank 0's agreement
+    then fails, and it must end like a deadline does -- the column layout's line printed, exit
+    status 0 -- instead of raising out of the loop with no line."""
+    plan = {"col": (0.02, None, None), "2x4-multipath": (0.0, {0: "raise", 1: "die"}, None),
+            "never": (0.0, None, None)}
+    res = _run(plan, tmp_path, timeout_s=30.0)
+    assert list(res) == [0]
+    line = res[0]
+    assert line["tag"] == "col"
+    assert line["config"]["autotune_ms_per_step"]["2x4-multipath"] == "timeout"
 
 
 if __name__ == "__main__":
