@@ -542,23 +542,18 @@ def main(argv=None):
         layout = (pdist.choose_layout(lw, n, F, nnz_bound, esz, mem) if args.layout == "auto"
                   else pdist.Layout.parse(args.layout, lw))
         cands = [(layout, args.overlap, args.exchange)]
+    # The default process group is gloo over host memory: the control plane (barriers, max
+    # over ranks, the failure agreement), which an RCCL failure cannot poison.  RCCL carries
+    # only the data-path exchange of layouts with row groups, on a group of its own that the
+    # first such candidate brings up (pdist.ensure_data_group), inside that candidate's
+    # deadline -- so an RCCL that fails to initialise, or stalls, costs that candidate, and the
+    # exchange-free column layout measured first still gives the line.  The groups' own
+    # watchdog (10 min) outlasts --candidate-timeout, so run_candidates ends a stall first.
+    rows = any(c[0].rows > 1 for c in cands)
+    data_backend = os.environ.get("PPNP_DIST_BACKEND") or ("nccl" if rows else "gloo")
     if world > 1:
-        # RCCL only where a layout has a data-path exchange (row groups); pure column layouts
-        # have none, so their control plane (barrier, max-over-ranks) runs over gloo.  The
-        # process group's own watchdog (10 min) outlasts --candidate-timeout, so a stalled
-        # exchange is ended by run_candidates, which still prints a line
-        rows = any(c[0].rows > 1 for c in cands)
-        backend = os.environ.get("PPNP_DIST_BACKEND") or ("nccl" if rows else "gloo")
-        if backend == "nccl":
-            torch.distributed.init_process_group("nccl", device_id=dev,
-                                                 timeout=datetime.timedelta(minutes=10))
-        else:
-            torch.distributed.init_process_group(backend)
-    # control plane (barriers, max over ranks, failure agreement) on gloo over host memory:
-    # RCCL carries only the data-path exchange
-    ctl = None
-    if world > 1 and torch.distributed.get_backend() == "nccl":
-        ctl = torch.distributed.new_group(backend="gloo")
+        torch.distributed.init_process_group("gloo", timeout=datetime.timedelta(minutes=10))
+    ctl = None  # the default (gloo) group
 
     t0 = time.perf_counter()
     indptr, indices = synth.graph_for(args.workload, device=dev)
@@ -684,6 +679,8 @@ def main(argv=None):
 
     def measure(cand):
         layout, overlap, exchange = cand
+        if world > 1 and layout.rows > 1:
+            pdist.ensure_data_group(data_backend, dev)  # collective; RCCL comes up here
         t1 = time.perf_counter()
         runner = pdist.PartitionedAPPNP.create(indptr, indices, n, H, K, alpha, dev,
                                                layout=layout, overlap=overlap,

@@ -95,8 +95,46 @@ def line_ld(width: int, elem_bytes: int = 4) -> int:
     return packed
 
 
+# The process group that carries the data-path exchange (RCCL all-gathers and P2P).  None: the
+# default group.  bench.py keeps the default group on gloo -- the control plane: barriers,
+# max-over-ranks, failure agreement, which no RCCL failure can poison -- and creates an RCCL
+# group for the exchange only when the first exchange candidate runs (``ensure_data_group``),
+# inside that candidate's deadline, so an RCCL that fails to come up costs that candidate and
+# not the run.
+_DATA_GROUP = None
+
+
+def data_group():
+    return _DATA_GROUP
+
+
+def data_backend():
+    """Backend of the data-path group ('nccl' = RCCL, 'gloo'), None without a process group."""
+    if not dist.is_initialized():
+        return None
+    return dist.get_backend(_DATA_GROUP) if _DATA_GROUP is not None else dist.get_backend()
+
+
+def ensure_data_group(backend: str, device) -> None:
+    """Create the data-path group over every rank once (collective: every rank calls it at the
+    same point), and bring its communicator up with a one-element all-reduce, so that a caller
+    reading the RCCL communicator (NativeRowAPPNP) finds it built.  No-op when the default group
+    already has that backend."""
+    global _DATA_GROUP
+    if _DATA_GROUP is not None or not dist.is_initialized() or dist.get_backend() == backend:
+        return
+    kw = {"device_id": torch.device(device)} if backend == "nccl" else {}
+    pg = dist.new_group(backend=backend, **kw)
+    t = torch.zeros(1, device=device if backend == "nccl" else "cpu")
+    dist.all_reduce(t, group=pg)
+    if t.is_cuda:
+        torch.cuda.synchronize(t.device)
+    _DATA_GROUP = pg
+
+
 class _TorchComm:
-    """In-place all-gather of equal row shards within a column group (RCCL for 'nccl')."""
+    """In-place all-gather of equal row shards within a column group (RCCL for 'nccl'), on the
+    data-path group (``data_group``)."""
 
     name = "group"
 
@@ -105,13 +143,14 @@ class _TorchComm:
         self.groups = {}
         ri, ci = layout.coords(rank)
         self.ri, self.ci = ri, ci
-        if layout.rows > 1:
+        self.backend = data_backend()
+        self.group = _DATA_GROUP
+        if layout.rows > 1 and layout.cols > 1:
             for c in range(layout.cols):
                 members = [c * layout.rows + r for r in range(layout.rows)]
-                g = dist.new_group(members) if layout.cols > 1 else None
+                g = dist.new_group(members, backend=self.backend)
                 if c == ci:
                     self.group = g
-        self.backend = dist.get_backend() if dist.is_initialized() else None
 
     def all_gather_rows(self, full: torch.Tensor, shard_rows: int, async_op: bool):
         """full: [R * shard_rows, ld]; this rank's shard already sits at row ri*shard_rows."""
@@ -180,7 +219,8 @@ class MultipathComm:
         self.widths = widths
         self.P = layout.size
         self.ri, self.ci = layout.coords(rank)
-        self.backend = dist.get_backend() if dist.is_initialized() else None
+        self.backend = data_backend()
+        self.group = _DATA_GROUP  # every rank relays: the whole data-path group
         self._stream = None
         self._staging = None
 
@@ -274,9 +314,9 @@ class MultipathComm:
                 bufs.append((kind, t, buf))
             fn = dist.isend if kind == "send" else dist.irecv
             if self.backend == "nccl":
-                ops.append(dist.P2POp(fn, buf, peer, tag=origin))
+                ops.append(dist.P2POp(fn, buf, peer, group=self.group, tag=origin))
             else:
-                ops.append(fn(buf, peer, tag=origin))
+                ops.append(fn(buf, peer, group=self.group, tag=origin))
         if self.backend == "nccl":
             works = dist.batch_isend_irecv(ops) if ops else []
         else:
@@ -610,14 +650,14 @@ class NativeRowAPPNP:
         self.device = torch.device(device)
         self.rank = dist.get_rank() if rank is None else rank
         self.world = dist.get_world_size() if world is None else world
-        backend = dist.get_backend() if dist.is_initialized() else None
+        backend = data_backend()
         self.exchange = exchange or ("rccl" if backend == "nccl" else "gloo")
         self._ws = None
         ctx = None
         if self.world == 1:
             fn = None
         elif self.exchange == "rccl":
-            pg = dist.distributed_c10d._get_default_group()
+            pg = _DATA_GROUP or dist.distributed_c10d._get_default_group()
             ctx = C.c_void_p(pg._get_backend(self.device)._comm_ptr())
             fn = _lib.ALLGATHER_FN(C.cast(lib.appnp_allgather_rccl, C.c_void_p).value)
         elif self.exchange == "gloo":

@@ -10,7 +10,10 @@ single-GPU appnp_propagate of the whole graph on its own device.  Backend gloo (
 share one GPU; the exchange callback stages the shards through host memory), or nccl with
 PPNP_DIST_BACKEND=nccl: then the exchange is appnp_allgather_rccl on torch's own
 communicator, and at world size 1 the worker also calls appnp_allgather_rccl directly once,
-which checks that the library resolves the process's RCCL.  Exit status 1 on mismatch.
+which checks that the library resolves the process's RCCL.  PPNP_DIST_BACKEND=gloo+nccl is
+bench.py's arrangement: a gloo default group for the control plane and an RCCL group for the
+data path (ppnp_amd.dist.ensure_data_group), whose communicator the engine then uses.  Exit
+status 1 on mismatch.
 """
 
 import argparse
@@ -51,6 +54,9 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
     else:
         dist.init_process_group("gloo")
+    if backend == "gloo+nccl":
+        pdist.ensure_data_group("nccl", dev)
+        assert pdist.data_backend() == "nccl" and dist.get_backend() == "gloo"
     rank, world = dist.get_rank(), dist.get_world_size()
     n, m, F, K, alpha, _ = synth.CONFIGS[a.workload]
     F = a.features or F
@@ -79,10 +85,10 @@ def main():
     want_split = a.split and a.sb_oom_rank < 0
     ok = err <= tol and (split_ran == want_split or runner.hi == runner.lo)
     extra = f" split={split_ran}"
-    if backend == "nccl" and world == 1:
+    if backend in ("nccl", "gloo+nccl") and world == 1:
         # the library's RCCL callback on torch's communicator: a one-rank in-place all-gather
         lib = _lib.load()
-        pg = dist.distributed_c10d._get_default_group()
+        pg = pdist.data_group() or dist.distributed_c10d._get_default_group()
         comm = pg._get_backend(dev)._comm_ptr()
         buf = torch.arange(1024, dtype=torch.float32, device=dev)
         before = buf.clone()
@@ -92,6 +98,12 @@ def main():
         torch.cuda.synchronize()
         ok = ok and rc == 0 and torch.equal(buf, before)
         extra += f" rccl_callback rc={rc}"
+        # torch's own in-place all-gather on the data-path group (the _TorchComm call)
+        full = torch.arange(64, dtype=torch.float32, device=dev)
+        dist.all_gather_into_tensor(full, full[:64], group=pdist.data_group())
+        torch.cuda.synchronize()
+        ok = ok and torch.equal(full, torch.arange(64, dtype=torch.float32, device=dev))
+        ok = ok and runner.exchange == "rccl"
     runner.close()
     print(f"[dist_capi] rank {rank}/{world} backend={dist.get_backend()} "
           f"exchange={runner.exchange} overlap={a.overlap} dtype={a.dtype} p_drop={a.p_drop} "

@@ -303,11 +303,14 @@ def test_native_row_engine_matches_single_gpu(ranks, extra):
     assert res == {r: "OK" for r in range(ranks)}, proc.stdout[-4000:]
 
 
-def test_native_row_engine_rccl_callback_one_rank():
+@pytest.mark.parametrize("backend", ["nccl", "gloo+nccl"])
+def test_native_row_engine_rccl_callback_one_rank(backend):
     """appnp_allgather_rccl resolves the RCCL PyTorch loaded and runs on its communicator
     (one rank: RCCL refuses two ranks on one device), and the engine's one-rank run agrees
-    with appnp_propagate."""
-    env = dict(os.environ, PPNP_DIST_BACKEND="nccl", PYTHONPATH=ROOT)
+    with appnp_propagate.  'gloo+nccl' is bench.py's arrangement: gloo default group, RCCL
+    data-path group brought up by ppnp_amd.dist.ensure_data_group; the engine, the library's
+    callback and torch's in-place all-gather all run on that group's communicator."""
+    env = dict(os.environ, PPNP_DIST_BACKEND=backend, PYTHONPATH=ROOT)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
            os.path.join(ROOT, "tests", "dist_capi_worker.py")]
