@@ -285,6 +285,30 @@ def test_bench_eight_ranks_every_candidate():
     assert 0 < rl["frac"] <= rl["ceiling"]["frac"] <= 1.0
 
 
+def test_bench_rccl_refused_still_prints_the_column_line():
+    """The driver's N = 2 command exactly as the driver runs it (no backend override), on the
+    one GPU: RCCL refuses two ranks on one device, so the data-path group cannot come up.  Since
+    that group is created inside the exchange candidates (dist.ensure_data_group), they fail,
+    are agreed failed over the gloo control plane and recorded as null, and the exchange-free
+    column layout's line is printed with exit status 0 (before round 3's second session,
+    init_process_group('nccl') at start-up ended the run with no line)."""
+    import json
+
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
+    env.pop("PPNP_DIST_BACKEND", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--workload", "arxiv-synth",
+           "--steps", "2", "--warmup", "1", "--candidate-timeout", "120"]
+    proc = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=280)
+    assert proc.returncode == 0, proc.stdout[-3000:] + proc.stderr[-3000:]
+    res = json.loads([l for l in proc.stdout.splitlines() if l.startswith("{")][-1])
+    tried = res["config"]["autotune_ms_per_step"]
+    assert res["config"]["parallelism"] == "rows1xcols2" and res["parity"]["ok"]
+    assert isinstance(tried["rows1xcols2"], float)
+    assert all(v is None for k, v in tried.items() if k != "rows1xcols2"), tried
+
+
 @pytest.mark.parametrize("ranks,extra", [
     (2, ["--overlap"]), (2, []), (3, ["--overlap", "--p-drop", "0.3"]),
     (2, ["--dtype", "bf16"]), (4, ["--workload", "arxiv-synth", "--overlap"])])
