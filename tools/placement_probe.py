@@ -26,6 +26,9 @@ def main():
     ap.add_argument("--calls", type=int, default=5)
     ap.add_argument("--hipmalloc", action="store_true",
                     help="allocate each workspace with its own hipMalloc (not torch's cache)")
+    ap.add_argument("--flags", type=int, default=None,
+                    help="allocate each workspace with hipExtMallocWithFlags(flags), e.g. 4 = "
+                         "hipDeviceMallocContiguous (physically contiguous: largest TLB fragments)")
     args = ap.parse_args()
 
     import ppnp_amd
@@ -48,7 +51,7 @@ def main():
     sp = C.c_void_p(stream.cuda_stream)
 
     hip = None
-    if args.hipmalloc:
+    if args.hipmalloc or args.flags is not None:
         hip = C.CDLL("libamdhip64.so")
 
     def alloc():
@@ -56,7 +59,11 @@ def main():
             t = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
             return t, t.data_ptr()
         p = C.c_void_p()
-        assert hip.hipMalloc(C.byref(p), C.c_size_t(ws_bytes)) == 0
+        if args.flags is not None:
+            rc = hip.hipExtMallocWithFlags(C.byref(p), C.c_size_t(ws_bytes), C.c_uint(args.flags))
+        else:
+            rc = hip.hipMalloc(C.byref(p), C.c_size_t(ws_bytes))
+        assert rc == 0, f"allocation failed: {rc}"
         return p, p.value
 
     def call(ptr):
