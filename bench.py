@@ -498,7 +498,8 @@ class SingleRunner:
 
 def cand_name(cand):
     layout, overlap, exchange = cand
-    return (f"rows{layout.rows}xcols{layout.cols}" + ("-overlap" if overlap else "")
+    return (f"rows{layout.rows}xcols{layout.cols}" + ("-lines" if layout.lines else "")
+            + ("-overlap" if overlap else "")
             + (f"-{exchange}" if (layout.rows > 1 and layout.cols > 1) or exchange == "native"
                else ""))
 

@@ -53,7 +53,7 @@ def _oracle_step(runner, src, out_rows, k, part):
         out_rows[:, :w] = torch.from_numpy(a * (g.rows_csr @ Zin) + runner.alpha * H).float()
 
 
-def _worker(rank, world, port, layout_spec, overlap, q, exchange="multipath"):
+def _worker(rank, world, port, layout_spec, overlap, q, exchange="multipath", f=F):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -62,7 +62,7 @@ def _worker(rank, world, port, layout_spec, overlap, q, exchange="multipath"):
 
         adj = O.synth_graph(N, 4 * N, seed=5)
         a_hat = O.calc_a_hat(adj, "sym")
-        H = torch.randn(N, F, generator=torch.Generator().manual_seed(0))
+        H = torch.randn(N, f, generator=torch.Generator().manual_seed(0))
         layout = Layout.parse(layout_spec, world)
         runner = PartitionedAPPNP.create(
             None, None, N, H, K, ALPHA, "cpu", layout=layout, overlap=overlap,
@@ -85,20 +85,23 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world,layout,overlap,exchange", [
-    (2, "row", False, "group"), (2, "row", True, "group"), (2, "col", False, "group"),
-    (2, "1x2", False, "group"),
+@pytest.mark.parametrize("world,layout,overlap,exchange,f", [
+    (2, "row", False, "group", F), (2, "row", True, "group", F), (2, "col", False, "group", F),
+    (2, "1x2", False, "group", F),
     # R x C layouts: two-stage relayed exchange over every rank (MultipathComm) and the
     # plain column-group all-gather
-    (8, "2x4", True, "multipath"), (8, "2x4", False, "multipath"), (8, "4x2", True, "multipath"),
-    (4, "2x2", False, "multipath"), (8, "2x4", True, "group")])
-def test_partitioned_matches_oracle(world, layout, overlap, exchange):
+    (8, "2x4", True, "multipath", F), (8, "2x4", False, "multipath", F),
+    (8, "4x2", True, "multipath", F),
+    (4, "2x2", False, "multipath", F), (8, "2x4", True, "group", F),
+    # column slabs cut at whole lines: 40 = 32 | 8, 100 = 32 | 32 | 36
+    (2, "col-lines", False, "group", 40), (3, "col-lines", False, "group", 100)])
+def test_partitioned_matches_oracle(world, layout, overlap, exchange, f):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    mp.start_processes(_worker, args=(world, _free_port(), layout, overlap, q, exchange),
+    mp.start_processes(_worker, args=(world, _free_port(), layout, overlap, q, exchange, f),
                        nprocs=world, join=True, start_method="spawn")
     res = sorted(q.get() for _ in range(world))
-    covered = np.zeros((N, F), dtype=bool)
+    covered = np.zeros((N, f), dtype=bool)
     for rank, lo, hi, flo, fhi, err in res:
         assert err < 1e-5, (rank, err)
         covered[lo:hi, flo:fhi] = True
@@ -126,9 +129,12 @@ def test_layout_helpers():
 
     # the north_star's pure row partition (overlapped all-gather) is timed at every N >= 2,
     # driven from Python and by the library's own loop (appnp_dist_*)
+    # ... and the column layout cut at whole lines, where that differs from the even cut
     assert candidate_layouts(2, 100) == [(Layout(1, 2), False, "group"),
+                                         (Layout(1, 2, True), False, "group"),
                                          (Layout(2, 1), True, "group"),
                                          (Layout(2, 1), True, "native")]
+    assert (Layout(1, 2, True), False, "group") not in candidate_layouts(2, 128)  # 64 | 64
     c8 = candidate_layouts(8, 100)
     assert c8[0] == (Layout(1, 8), False, "group") and (Layout(2, 4), True, "multipath") in c8
     assert (Layout(8, 1), True, "group") in c8 and (Layout(8, 1), True, "native") in c8
@@ -138,9 +144,29 @@ def test_layout_helpers():
         assert (lay, True, "multipath") in c8 and (lay, True, "group") in c8
     assert len(c8) == len(set(c8)) == 7
     c4 = candidate_layouts(4, 100)
-    assert c4 == [(Layout(1, 4), False, "group"), (Layout(2, 2), True, "multipath"),
+    assert c4 == [(Layout(1, 4), False, "group"), (Layout(1, 4, True), False, "group"),
+                  (Layout(2, 2), True, "multipath"),
                   (Layout(2, 2), True, "group"), (Layout(4, 1), True, "group"),
                   (Layout(4, 1), True, "native")]
+
+
+def test_line_slabs():
+    """Column slabs cut at whole 128-B lines: whole lines first, the remainder on the last
+    slab (which holds the fewest lines); None when a slab would be empty."""
+    from ppnp_amd.dist import Layout, line_slab_cols, slab_range
+
+    assert line_slab_cols(100, 2) == [(0, 64), (64, 100)]
+    assert line_slab_cols(100, 3) == [(0, 32), (32, 64), (64, 100)]
+    assert line_slab_cols(100, 4) == [(0, 32), (32, 64), (64, 96), (96, 100)]
+    assert line_slab_cols(100, 5) is None and line_slab_cols(100, 8) is None
+    assert line_slab_cols(128, 4) == [(0, 32), (32, 64), (64, 96), (96, 128)]
+    assert line_slab_cols(128, 5) is None and line_slab_cols(13, 2) is None
+    assert line_slab_cols(100, 2, 2) == [(0, 64), (64, 100)]  # bf16: 64 columns per line
+    assert Layout.parse("col-lines", 4) == Layout(1, 4, True)
+    assert [slab_range(100, Layout(1, 4, True), c) for c in range(4)] == line_slab_cols(100, 4)
+    assert slab_range(100, Layout(1, 4), 3) == (75, 100)
+    with pytest.raises(ValueError):
+        slab_range(100, Layout(1, 8, True), 0)
 
 
 def test_layout_memory_and_index_limits():
