@@ -219,6 +219,26 @@ def test_arxiv_row_partition_matches_oracle(ranks, extra):
     assert res == {r: "OK" for r in range(ranks)}, proc.stdout[-4000:]
 
 
+@pytest.mark.parametrize("ranks", [2, 4])
+def test_line_cut_column_slabs_match_oracle(ranks):
+    """Column slabs cut at whole lines (dist.line_slab_cols; the autotune candidate that wins
+    on 2 ranks): F = 100 as 64 | 36 (the 36-column slab on the split path: 32 + a 4-column
+    remainder pass) and 32 | 32 | 32 | 4 (a narrow slab wholly in the pass), real HIP kernels on
+    a 200k-node graph, each rank's block against the float64 oracle."""
+    env = dict(os.environ, PPNP_DIST_BACKEND="gloo", PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={ranks}", "--master-addr=127.0.0.1",
+           f"--master-port={_free_port()}", os.path.join(ROOT, "tests", "dist_worker.py"),
+           "--layout", "col-lines", "--f", "100", "--graph-n", "200000", "--graph-m", "1000000",
+           "--K", "4", "--oracle"]
+    proc = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=200)
+    assert proc.returncode == 0, proc.stdout[-3000:] + proc.stderr[-3000:]
+    res = _rank_results(proc.stdout, "dist_worker")
+    assert res == {r: "OK" for r in range(ranks)}, proc.stdout[-4000:]
+    lines = [l for l in proc.stdout.splitlines() if l.startswith("[dist_worker]")]
+    assert any("split_cols=4" in l for l in lines), lines  # the last slab took the pass
+
+
 def test_stream_done_orders_consumer_after_side_stream():
     """The hand-off of the relayed exchange (dist.MultipathComm on 'nccl'): work queued on a
     side stream, then _StreamDone.wait() on the caller's stream -- a consumer queued after the
