@@ -327,7 +327,10 @@ typedef int (*appnp_allgather_fn)(void* buf, size_t shard_bytes, int rank, int n
  * none: the rule is the same on every rank (its gather-locality measure is taken over the whole
  * A), and since the copy is best-effort, the first fp32 propagation with K >= 2 agrees through
  * one small exchange in the workspace that every rank built it (that call synchronises the
- * stream once).  H and Z must allow 16-B vectors on every rank alike.
+ * stream once), and a rank whose agreement fails keeps failing (the handle is poisoned: every
+ * later call returns the error).  ld_h and ld_z must be the same on every rank: with both a
+ * multiple of 4 the split layout runs, and a rank whose H or Z is then not 16-B aligned gets
+ * APPNP_EINVAL (its peers would split); otherwise every rank gathers whole rows.
  * overlap != 0 keeps the held rows as local- and remote-column CSRs (fp32 propagation only).
  * allgather/ctx: the exchange, called by every rank once per exchanged iterate (twice on the
  * split layout: its main part, then its remainder part). */
@@ -362,6 +365,18 @@ void appnp_dist_destroy(appnp_dist* d);
  * APPNP_ENOTSUP if it cannot be loaded, APPNP_EDEVICE if the call fails. */
 int appnp_allgather_rccl(void* buf, size_t shard_bytes, int rank, int nranks, void* stream,
                          void* ctx);
+
+/*
+ * Measurement aid (no counterpart in the reference): gathers `lines` random 128-B lines of the
+ * device buffer `table` (table_bytes, 128-B aligned; read only) on `stream`, 8 lanes per line
+ * and 64 lines in flight per wave, line indices hashed from `seed`.  The caller times it with
+ * events; lines / time is the box's random-line rate, the quantity that bounds the SpMM on a
+ * uniform random graph.  bench.py runs it before its timed region
+ * (roofline.box_line_rate).  `sink`: one device float, written only if the gathered sum hits a
+ * sentinel value.
+ */
+int appnp_line_rate_probe(const void* table, int64_t table_bytes, int64_t lines, uint64_t seed,
+                          float* sink, void* stream);
 
 #ifdef __cplusplus
 }

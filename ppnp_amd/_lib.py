@@ -95,6 +95,7 @@ _SIGS = {
     ),
     "appnp_dist_destroy": (None, [_vp]),
     "appnp_allgather_rccl": (_i32, [_vp, _sz, _i32, _i32, _vp, _vp]),
+    "appnp_line_rate_probe": (_i32, [_vp, _i64, _i64, _u64, _vp, _vp]),
     "appnp_step": (
         _i32,
         [_vp, _i32, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _f32,

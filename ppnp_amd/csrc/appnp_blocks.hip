@@ -77,6 +77,17 @@ constexpr int kRemChunk = kWave;                // entries per chunk; segments p
 #define APPNP_REM_U 2
 #endif
 constexpr int kRemU = APPNP_REM_U;              // chunks in flight per wave (-DAPPNP_REM_U: measurement)
+// W8 / W16 passes (16 / 32 entries per chunk): 4 chunks in flight.  The 13-column slab of
+// products-synth (W16) took 1.93 ms at 4, 1.94 at 8, 2.01 at 2 and 2.25 at 1
+// (profiles/r4_w16_ab.txt)
+#ifndef APPNP_REM_U_WIDE
+#define APPNP_REM_U_WIDE 4
+#endif
+constexpr int kRemUWide = APPNP_REM_U_WIDE;
+#ifndef APPNP_REM_SYNC_MASK
+#define APPNP_REM_SYNC_MASK 0
+#endif
+constexpr int kRemSyncMask = APPNP_REM_SYNC_MASK;
 
 static_assert(kRemMaxRg < (1 << kRemRowBits), "row in group must fit the packed entry");
 static_assert(kRemRowBits + kRemColBits == 32, "packed entry is 32 bits");
@@ -245,85 +256,110 @@ __device__ __forceinline__ void rem_finish_piece(const StepArgs& a, const RemLay
   }
 }
 
+// Chunks [c_begin, c_end) of a wave's entry stream: gather, weight, segmented scan, and the
+// run tails' adds into the wave's LDS rows.  U chunks in flight; the source block of chunk c is
+// cblk[c].
+template <int U, bool VF, int LPE>
+__device__ __forceinline__ void rem_walk(const StepArgs& a, const RemLayout& L,
+                                         const f32x4* __restrict__ z, f32x4* acc, int64_t r0,
+                                         int32_t c_begin, int32_t c_end) {
+  constexpr int CH = kWave / LPE;  // entries per chunk; piece q of entry e on lane q * CH + e
+  const int lane = threadIdx.x & (kWave - 1);
+  const int q = lane / CH, le = lane % CH;
+  const uint32_t cmask = (1u << kRemColBits) - 1u;
+  for (int32_t c = c_begin; c < c_end; c += U) {
+    const int nch = min(U, c_end - c);
+    int32_t cb[U];  // first source row of each chunk's block (wave-uniform: scalar loads)
+    uint32_t en[U];
+    float wt[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      cb[u] = 0;
+      en[u] = kRemNone;
+      wt[u] = 1.0f;
+      if (u < nch) {
+        const int64_t e = (int64_t)(c + u) * CH + le;
+        cb[u] = L.cblk[c + u] << L.br_log2;
+        en[u] = ld_nt<uint32_t>(L.ent + e);
+        if constexpr (!VF) wt[u] = ld_nt<float>(L.val + e);
+      }
+    }
+    f32x4 zv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if constexpr (LPE == 1) {
+        zv[u] = en[u] != kRemNone ? z[cb[u] + (int32_t)(en[u] & cmask)]
+                                  : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+      } else {
+        // a piece wholly past the valid remainder columns (a.f) holds zeros in every buffer:
+        // no request for it (a 4-column remainder on a W8 / W16 copy gathers one piece)
+        zv[u] = (en[u] != kRemNone && 4 * q < a.f)
+                    ? z[(int64_t)(cb[u] + (int32_t)(en[u] & cmask)) * LPE + q]
+                    : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (u >= nch) break;  // wave-uniform
+      const bool act = en[u] != kRemNone;
+      const int row = (int)(en[u] >> kRemColBits);
+      // scan key: the row, and for LPE > 1 the piece (runs never cross pieces)
+      const int key = LPE == 1 ? row : ((row << 3) | q);
+      f32x4 v = zv[u];
+      if (!VF || a.drop_on) {
+        const float w = act ? edge_weight(wt[u], a.row_lo + r0 + row,
+                                          cb[u] + (int32_t)(en[u] & cmask), a)
+                            : 0.0f;
+        v = f32x4{w * v.x, w * v.y, w * v.z, w * v.w};
+      }
+      // the previous lane's row (lane 0: none), by DPP rather than an LDS permute
+      const int prev = __builtin_amdgcn_update_dpp(-1, key, kDppWaveShr1, 0xf, 0xf, false);
+      const unsigned long long heads = __ballot(lane == 0 || prev != key || !act);
+      seg_scan<CH>(key, v, heads);
+      const bool tail = le == CH - 1 || ((heads >> (lane + 1)) & 1ull);
+      if (act && tail) {
+        const f32x4 s = acc[row * LPE + q];
+        acc[row * LPE + q] = f32x4{s.x + v.x, s.y + v.y, s.z + v.z, s.w + v.w};
+      }
+    }
+  }
+}
+
 // One iteration of the remainder columns over all source blocks (see the file comment).
 // a.zin = Z_rem (n x 4 fp32; VF: dr o Z_rem); U chunks of 64 entries in flight per wave.
 // VF (unit graph): entries carry no value -- the sum of the gathered dr_j Z_j is scaled by
 // dl_i in the epilogue, so the entry stream is 4 B per entry instead of 8 (0.91 -> 0.81 ms
 // per products-synth launch).
-template <int EPI, int U, bool VF, int LPE>
+// SYNC: the waves of a workgroup walk the source blocks in step, with a workgroup barrier after
+// every block.  Without it a wave streams its segments back to back, and the CU's oldest-first
+// arbitration spreads its waves over ~12 % of the sweep (profiles/r3_rem_timeline.txt): that
+// span of blocks must share the XCD's 4 MB L2, which a W4 table's 512-KB blocks do (92 % hits)
+// and a W16 table's 2-MB blocks do not (28 %; profiles/r4_w16_*).
+template <int EPI, int U, bool VF, int LPE, bool SYNC>
 __global__ __launch_bounds__(kRemThreads) void k_rem_persist(StepArgs a, RemLayout L) {
-  constexpr int CH = kWave / LPE;  // entries per chunk; piece q of entry e on lane q * CH + e
+  constexpr int CH = kWave / LPE;
   extern __shared__ f32x4 rem_acc[];
   const int lane = threadIdx.x & (kWave - 1);
-  const int q = lane / CH, le = lane % CH;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   f32x4* acc = rem_acc + (int64_t)wv * L.rg * LPE;
   const f32x4* __restrict__ z = static_cast<const f32x4*>(a.zin);
   const int64_t slot = (int64_t)blockIdx.x * kRemWaves + wv;
-  const uint32_t cmask = (1u << kRemColBits) - 1u;
   for (int p = 0; p < L.passes; ++p) {
     const int64_t g = (int64_t)p * L.slots + slot;
     const int64_t r0 = g * L.rg;
     const int rows = (int)max<int64_t>(0, min<int64_t>(L.rg, a.n_rows - r0));
     for (int r = lane; r < rows * LPE; r += kWave) acc[r] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    // this wave's stream: blocks 0..nb-1 back to back, each a whole number of chunks; the
-    // block of chunk c is cblk[c]
-    const int32_t c_end = L.off[(g + 1) * L.nb] / CH;
-    for (int32_t c = L.off[g * L.nb] / CH; c < c_end; c += U) {
-      const int nch = min(U, c_end - c);
-      int32_t cb[U];  // first source row of each chunk's block (wave-uniform: scalar loads)
-      uint32_t en[U];
-      float wt[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        cb[u] = 0;
-        en[u] = kRemNone;
-        wt[u] = 1.0f;
-        if (u < nch) {
-          const int64_t e = (int64_t)(c + u) * CH + le;
-          cb[u] = L.cblk[c + u] << L.br_log2;
-          en[u] = ld_nt<uint32_t>(L.ent + e);
-          if constexpr (!VF) wt[u] = ld_nt<float>(L.val + e);
-        }
+    if constexpr (SYNC) {
+      // every wave runs the same nb blocks (an empty segment is 0 chunks), so every wave
+      // reaches every barrier
+      for (int b = 0; b < L.nb; ++b) {
+        rem_walk<U, VF, LPE>(a, L, z, acc, r0, L.off[g * L.nb + b] / CH,
+                             L.off[g * L.nb + b + 1] / CH);
+        __syncthreads();
       }
-      f32x4 zv[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if constexpr (LPE == 1) {
-          zv[u] = en[u] != kRemNone ? z[cb[u] + (int32_t)(en[u] & cmask)]
-                                    : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-        } else {
-          // a piece wholly past the valid remainder columns (a.f) holds zeros in every buffer:
-          // no request for it (a 4-column remainder on a W8 / W16 copy gathers one piece)
-          zv[u] = (en[u] != kRemNone && 4 * q < a.f)
-                      ? z[(int64_t)(cb[u] + (int32_t)(en[u] & cmask)) * LPE + q]
-                      : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (u >= nch) break;  // wave-uniform
-        const bool act = en[u] != kRemNone;
-        const int row = (int)(en[u] >> kRemColBits);
-        // scan key: the row, and for LPE > 1 the piece (runs never cross pieces)
-        const int key = LPE == 1 ? row : ((row << 3) | q);
-        f32x4 v = zv[u];
-        if (!VF || a.drop_on) {
-          const float w = act ? edge_weight(wt[u], a.row_lo + r0 + row,
-                                            cb[u] + (int32_t)(en[u] & cmask), a)
-                              : 0.0f;
-          v = f32x4{w * v.x, w * v.y, w * v.z, w * v.w};
-        }
-        // the previous lane's row (lane 0: none), by DPP rather than an LDS permute
-        const int prev = __builtin_amdgcn_update_dpp(-1, key, kDppWaveShr1, 0xf, 0xf, false);
-        const unsigned long long heads = __ballot(lane == 0 || prev != key || !act);
-        seg_scan<CH>(key, v, heads);
-        const bool tail = le == CH - 1 || ((heads >> (lane + 1)) & 1ull);
-        if (act && tail) {
-          const f32x4 c = acc[row * LPE + q];
-          acc[row * LPE + q] = f32x4{c.x + v.x, c.y + v.y, c.z + v.z, c.w + v.w};
-        }
-      }
+    } else {
+      // this wave's stream: blocks 0..nb-1 back to back, each a whole number of chunks
+      rem_walk<U, VF, LPE>(a, L, z, acc, r0, L.off[g * L.nb] / CH, L.off[(g + 1) * L.nb] / CH);
     }
     if constexpr (LPE == 1) {
       for (int r = lane; r < rows; r += kWave) rem_finish<EPI, VF>(a, L, r0 + r, acc[r]);
@@ -470,24 +506,41 @@ __global__ __launch_bounds__(kBlock) void k_split_copy(const float* __restrict__
   }
 }
 
-template <int EPI, bool VF, int LPE>
+template <int EPI, bool VF, int LPE, bool SYNC>
 hipError_t launch_rem(dim3 grid, dim3 block, size_t lds, hipStream_t s, const StepArgs& a,
                       const RemLayout& L) {
+  constexpr int U = LPE == 1 ? kRemU : kRemUWide;
   static const hipError_t attr = hipFuncSetAttribute(  // > 64 KiB of dynamic LDS, once
-      reinterpret_cast<const void*>(k_rem_persist<EPI, kRemU, VF, LPE>),
+      reinterpret_cast<const void*>(k_rem_persist<EPI, U, VF, LPE, SYNC>),
       hipFuncAttributeMaxDynamicSharedMemorySize, kRemLdsBytes);
   if (attr != hipSuccess) return attr;
-  hipLaunchKernelGGL((k_rem_persist<EPI, kRemU, VF, LPE>), grid, block, lds, s, a, L);
+  hipLaunchKernelGGL((k_rem_persist<EPI, U, VF, LPE, SYNC>), grid, block, lds, s, a, L);
   return hipGetLastError();
+}
+
+int env_or(const char* name, int dflt);
+
+// Widths whose pass walks the source blocks in step (SYNC; bit LPE of the mask).
+// APPNP_REM_SYNC overrides the mask (measurement).
+int rem_sync_mask() {
+  static const int m = env_or("APPNP_REM_SYNC", kRemSyncMask);
+  return m;
 }
 
 template <int EPI, bool VF>
 hipError_t launch_rem_lpe(int lpe, dim3 grid, dim3 block, size_t lds, hipStream_t s,
                           const StepArgs& a, const RemLayout& L) {
+  const bool sync = (rem_sync_mask() >> lpe) & 1;
   switch (lpe) {
-    case 1: return launch_rem<EPI, VF, 1>(grid, block, lds, s, a, L);
-    case 2: return launch_rem<EPI, VF, 2>(grid, block, lds, s, a, L);
-    case 4: return launch_rem<EPI, VF, 4>(grid, block, lds, s, a, L);
+    case 1:
+      return sync ? launch_rem<EPI, VF, 1, true>(grid, block, lds, s, a, L)
+                  : launch_rem<EPI, VF, 1, false>(grid, block, lds, s, a, L);
+    case 2:
+      return sync ? launch_rem<EPI, VF, 2, true>(grid, block, lds, s, a, L)
+                  : launch_rem<EPI, VF, 2, false>(grid, block, lds, s, a, L);
+    case 4:
+      return sync ? launch_rem<EPI, VF, 4, true>(grid, block, lds, s, a, L)
+                  : launch_rem<EPI, VF, 4, false>(grid, block, lds, s, a, L);
     default: return hipErrorInvalidValue;
   }
 }

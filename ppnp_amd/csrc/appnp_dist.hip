@@ -43,6 +43,8 @@ struct appnp_dist {
   int sb_requested = 0;                // `mode` asked for the source-blocked copy (all ranks)
   int split_agreed = 0;                // the ranks have agreed on split_ok (first propagation)
   int split_ok = 0;                    // every rank holds its rows' source-blocked copy
+  int poisoned = APPNP_OK;             // the split agreement failed on this rank: every later
+                                       // call returns this code (the ranks may disagree now)
   hipStream_t xs = nullptr;            // exchange stream (overlap)
   hipEvent_t produced = nullptr;       // dst rows written on the caller's stream
   hipEvent_t exchanged = nullptr;      // exchange finished on xs
@@ -96,12 +98,17 @@ WsLayout ws_layout(const appnp_dist* d, int64_t f, int dtype) {
 // regrouped copy is best-effort: at the first fp32 propagation with K >= 2 of an engine whose
 // `mode` asked for the copy, the ranks agree through the exchange itself -- each sets one byte
 // of its slot of a small in-place all-gather in the workspace, and the copy is used only if
-// every rank built it.  Synchronises the stream once.
+// every rank built it.  Synchronises the stream once.  If the agreement itself fails on this
+// rank (exchange or copy error), its peers may have completed it and decided differently, so
+// the handle is poisoned: this and every later call returns the error instead of running a
+// loop that exchanges a different number of parts than the peers' (ADVICE r3).
 int agree_split(appnp_dist* d, void* ws, hipStream_t s) {
   constexpr size_t kSlot = 256;
-  d->split_agreed = 1;
   d->split_ok = d->g->rb_off != nullptr;
-  if (d->nranks <= 1) return APPNP_OK;
+  if (d->nranks <= 1) {
+    d->split_agreed = 1;
+    return APPNP_OK;
+  }
   char* flags = static_cast<char*>(ws);
   std::vector<unsigned char> host((size_t)d->nranks, 0);
   int rc = dev_err(hipMemsetAsync(flags, 0, kSlot * d->nranks, s));
@@ -113,6 +120,8 @@ int agree_split(appnp_dist* d, void* ws, hipStream_t s) {
   if (rc == APPNP_OK) rc = dev_err(hipStreamSynchronize(s));
   for (int p = 0; p < d->nranks; ++p)
     if (rc != APPNP_OK || host[p] != 1) d->split_ok = 0;
+  if (rc != APPNP_OK) d->poisoned = rc;
+  d->split_agreed = 1;
   return rc;
 }
 
@@ -270,6 +279,7 @@ int appnp_dist_propagate(appnp_dist* d, const void* H, int64_t ld_h, void* Z, in
   if (d->overlap && dtype != APPNP_F32) return APPNP_ENOTSUP;
   if (!(alpha >= 0.0f && alpha <= 1.0f) || !(p_drop >= 0.0f && p_drop < 1.0f))
     return APPNP_EINVAL;
+  if (d->poisoned != APPNP_OK) return d->poisoned;
   const int64_t rows = d->hi - d->lo;
   if (f == 0) return APPNP_OK;
   if (rows > 0 && (!H || !Z || ld_h < f || ld_z < f)) return APPNP_EINVAL;
@@ -282,12 +292,13 @@ int appnp_dist_propagate(appnp_dist* d, const void* H, int64_t ld_h, void* Z, in
     const int arc = agree_split(d, ws, s);
     if (arc != APPNP_OK) return arc;
   }
-  // split rows when every rank's copy allows it and H / Z allow 16-B vectors (K >= 2: one
-  // iteration gains nothing from the split layout).  Collective: H and Z must allow 16-B
-  // vectors on every rank alike, as they do when every rank runs the same code
-  // (include/ppnp_amd.h)
-  if (d->split_ok && w.split_total && K >= 2 &&
-      (rows == 0 || (aligned16(H, ld_h) && aligned16(Z, ld_z)))) {
+  // split rows when every rank's copy allows it and the leading dimensions allow 16-B vectors
+  // (K >= 2: one iteration gains nothing from the split layout).  Collective: ld_h / ld_z are
+  // the same on every rank (include/ppnp_amd.h), so that part of the decision agrees; a base
+  // pointer that is not 16-B aligned is this rank's alone, and the rank reports it instead of
+  // silently exchanging one part per iterate where its peers exchange two
+  if (d->split_ok && w.split_total && K >= 2 && ld_h % 4 == 0 && ld_z % 4 == 0) {
+    if (rows > 0 && !(aligned16(H, ld_h) && aligned16(Z, ld_z))) return APPNP_EINVAL;
     if (!ws || ws_bytes < w.split_total) return APPNP_EINVAL;
     return propagate_split_rows(d, w, static_cast<const float*>(H), ld_h, static_cast<float*>(Z),
                                 ld_z, f, K, alpha, p_drop, seed, static_cast<char*>(ws), s);

@@ -304,13 +304,16 @@ class MultipathComm:
         return s1, s2, len(slots), max((hi - lo for lo, hi in pieces), default=0)
 
     def _width(self, origin: int, full) -> int:
+        """Columns of origin's slab a message carries: its column group's width (packed), or
+        the whole buffer row when no widths are given (every rank's buffers then agree)."""
         if self.widths is None:
             return full.shape[1]
-        return min(self.widths[origin // self.layout.rows], full.shape[1])
+        return self.widths[origin // self.layout.rows]
 
     def _views(self, full, shard_rows, ops, nslots, pmax):
         R = self.layout.rows
-        # staging slot s holds a piece of origin a's slab, packed at a's width
+        # staging slot s holds a piece of origin a's slab, packed at a's width -- which is not
+        # this relay's own width when a is in another column group (F = 73 on 2 x 2: 37 | 36)
         slot_w = {}
         for kind, peer, origin, (lo, hi), where in ops:
             if where != "full":
@@ -326,9 +329,9 @@ class MultipathComm:
             off += pmax * slot_w[slot]
         out = []
         for kind, peer, origin, (lo, hi), where in ops:
-            if where == "full":
+            if where == "full":  # origin is in this rank's column group: its own width
                 base = (origin % R) * shard_rows
-                t = full[base + lo:base + hi, :self._width(origin, full)]
+                t = full[base + lo:base + hi, :min(self._width(origin, full), full.shape[1])]
             else:
                 w = slot_w[where[1]]
                 o = offs[where[1]]
@@ -485,12 +488,7 @@ class PartitionedAPPNP:
             # groups and the regrouped copy is best-effort, so all ranks agree -- every rank
             # takes part, whatever it found
             if dist.is_initialized() and layout.size > 1:
-                on_gpu = dist.get_backend() == "nccl"
-                t = torch.tensor([1 if split else 0], dtype=torch.int32,
-                                 device=device if on_gpu else "cpu")
-                dist.all_reduce(t, op=dist.ReduceOp.MIN)
-                if not int(t.item()):
-                    split = None
+                split = agree_split(split, device)
         if split is None:
             bufs = [torch.zeros(rows_pad, ld, dtype=H.dtype, device=device) for _ in range(2)]
             partial = (torch.zeros(max(hi - lo, 0), ld, dtype=torch.float32, device=device)
@@ -644,6 +642,28 @@ class PartitionedAPPNP:
             work.wait()
         self.out = cur[lo:hi, :w]
         return self.out
+
+
+def agree_split(split, device, group=None):
+    """The split layout every rank of the (default) process group takes: this rank's ``split``
+    -- (fs, remainder width) or None -- if every rank found the SAME (fs, width), else None
+    (whole rows everywhere).  Collective.
+
+    Agreeing only on "split or not" is not enough: the exchanged parts are [rows, fs] and
+    [rows, width] buffers, and the relayed exchange (MultipathComm) sizes its staging and its
+    P2P messages from the rank's own buffers, so column groups whose slabs split differently --
+    F = 73 on 2 x 2 is 37 | 36 columns, i.e. a W8 copy (32 + 5) beside a W4 copy (32 + 4) --
+    would send and receive messages of different sizes.  One MIN all-reduce of
+    (split, fs, -fs, width, -width) gives the minimum and maximum of both."""
+    on_gpu = dist.get_backend(group) == "nccl"
+    fs, rw = split if split else (0, 0)
+    t = torch.tensor([1 if split else 0, fs, -fs, rw, -rw], dtype=torch.int64,
+                     device=device if on_gpu else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    ok, fs_min, fs_max, rw_min, rw_max = (int(x) for x in t.tolist())
+    if not ok or fs_min != -fs_max or rw_min != -rw_max:
+        return None
+    return split
 
 
 def _hip_step(runner: PartitionedAPPNP, src, out_rows, k, part):
@@ -838,16 +858,16 @@ INT32_MAX = 2**31 - 1
 
 
 def rank_bytes(layout: Layout, n: int, f: int, nnz_hat: int, elem_bytes: int = 4,
-               overlap: bool = False) -> int:
+               overlap: bool = False, width: int | None = None) -> int:
     """Device bytes one rank of ``layout`` holds for the K loop (upper estimate): its rows'
     CSR (int32 row_ptr, int32 col + fp32 val; doubled by the local/remote split of overlap
     mode; plus the source-blocked copy where a column slab takes the split-row path), dinv
     (fp64, all n), the H slab of its rows, two full-height Z slabs, and the fp32 partial of
-    overlap mode."""
+    overlap mode.  ``width``: the widest slab when the cut is not even (line slabs)."""
     R, C = layout.rows, layout.cols
     shard = -(-n // R)
     nnz_r = -(-nnz_hat // R)
-    width = -(-f // C)
+    width = width or -(-f // C)
     ld = line_ld(width, elem_bytes)
     csr = 4 * (shard + 1) + 8 * nnz_r
     if overlap:
@@ -865,7 +885,8 @@ def rank_bytes(layout: Layout, n: int, f: int, nnz_hat: int, elem_bytes: int = 4
 
 
 def fits(layout: Layout, n: int, f: int, nnz_hat: int, elem_bytes: int = 4,
-         overlap: bool = False, mem_bytes: int | None = None, headroom: float = 0.85) -> bool:
+         overlap: bool = False, mem_bytes: int | None = None, headroom: float = 0.85,
+         width: int | None = None) -> bool:
     """Whether a rank's share stays inside the int32 CSR index range and, given the device
     memory, inside ``headroom`` of it.  A feature-column layout replicates the whole CSR on
     every rank; only row groups split it (the north_star's 'graphs that outgrow one GPU')."""
@@ -873,7 +894,7 @@ def fits(layout: Layout, n: int, f: int, nnz_hat: int, elem_bytes: int = 4,
         return False
     if mem_bytes is None:
         return True
-    return rank_bytes(layout, n, f, nnz_hat, elem_bytes, overlap) <= headroom * mem_bytes
+    return rank_bytes(layout, n, f, nnz_hat, elem_bytes, overlap, width) <= headroom * mem_bytes
 
 
 def candidate_layouts(world: int, f: int, n: int = 0, nnz_hat: int = 0, elem_bytes: int = 4,
@@ -901,7 +922,9 @@ def candidate_layouts(world: int, f: int, n: int = 0, nnz_hat: int = 0, elem_byt
     # the column layout cut at whole lines (exchange-free too): fewer lines per gather on the
     # ranks that get whole lines, when that differs from the even cut
     lines = line_slab_cols(f, world, elem_bytes) if first == Layout(1, world) else None
-    if lines and lines != [col_range(f, world, c) for c in range(world)]:
+    if (lines and lines != [col_range(f, world, c) for c in range(world)]
+            and fits(Layout(1, world, True), n, f, nnz_hat, elem_bytes, False, mem_bytes,
+                     width=max(hi - lo for lo, hi in lines))):
         cands.append((Layout(1, world, True), False, "group"))
     if world >= 4 and world % 2 == 0:
         seen = {first}

@@ -224,3 +224,34 @@ class PropagatePlan:
             self.close()
         except Exception:
             pass
+
+
+def line_rate_probe(table: torch.Tensor, lines: int, seed: int = 0, reps: int = 3) -> dict:
+    """The device's random 128-B line rate (``appnp_line_rate_probe``): ``lines`` random lines
+    gathered from ``table``'s storage (read only) per launch, one warm-up launch, then the
+    median of ``reps`` launches timed with HIP events on the current stream.  Returns
+    {"G_lines_s", "ms", "lines", "table_MB"}."""
+    if not table.is_cuda:
+        raise ValueError("table must be a device tensor")
+    lib = _lib.load()
+    dev = table.device
+    base = table.untyped_storage().data_ptr()
+    nbytes = table.untyped_storage().nbytes()
+    skip = (-base) % 128  # the kernel gathers whole 128-B lines from a 128-B aligned start
+    tbytes = (nbytes - skip) // 128 * 128
+    sink = torch.zeros(1, dtype=torch.float32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    times = []
+    with torch.cuda.device(dev):
+        for r in range(reps + 1):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+            _lib.check("appnp_line_rate_probe", lib.appnp_line_rate_probe(
+                C.c_void_p(base + skip), tbytes, int(lines), int(seed + r) & (2**64 - 1),
+                C.c_void_p(sink.data_ptr()), C.c_void_p(stream.cuda_stream)))
+            b.record(stream)
+            times.append((a, b))
+        torch.cuda.synchronize(dev)
+    ms = sorted(a.elapsed_time(b) for a, b in times[1:])[reps // 2]
+    return {"G_lines_s": lines / (ms * 1e-3) / 1e9, "ms": ms, "lines": int(lines),
+            "table_MB": tbytes / 2**20}

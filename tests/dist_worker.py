@@ -32,7 +32,8 @@ def main():
     p.add_argument("--graph-n", dest="n", type=int, default=60000)
     p.add_argument("--graph-m", dest="m", type=int, default=400000)
     p.add_argument("--f", type=int, default=20)
-    p.add_argument("--K", type=int, default=10)
+    p.add_argument("--K", type=int, default=None, help="iterations (default 10, or the "
+                                                       "workload's K)")
     p.add_argument("--alpha", type=float, default=0.1)
     p.add_argument("--p-drop", type=float, default=0.0)
     p.add_argument("--workload", default=None,
@@ -41,6 +42,10 @@ def main():
     p.add_argument("--oracle", action="store_true",
                    help="compare with the float64 CPU oracle (oracle/ppnp_oracle.py) instead of "
                         "the single-GPU HIP propagation")
+    p.add_argument("--oracle-torch", action="store_true",
+                   help="compare with the oracle's float64 torch.sparse CPU loop over the device "
+                        "A_hat of a whole-graph build (products scale: tests/test_gpu_configs.py "
+                        "pins that A_hat to calc_a_hat entry by entry)")
     p.add_argument("--expect-split", type=int, default=None,
                    help="fail unless the rank's remainder columns (split rows) equal this")
     p.add_argument("--sb-oom-rank", type=int, default=-1,
@@ -64,9 +69,11 @@ def main():
         dist.init_process_group(backend)
     rank = dist.get_rank()
     if a.workload:
-        a.n, a.m, a.f, a.K, a.alpha, _ = synth.CONFIGS[a.workload]
+        a.n, a.m, a.f, K, a.alpha, _ = synth.CONFIGS[a.workload]
+        a.K = K if a.K is None else a.K
         indptr, indices = synth.graph_for(a.workload, device=dev)
     else:
+        a.K = 10 if a.K is None else a.K
         indptr, indices = synth.uniform_graph(a.n, a.m, 7, device=dev)
     H = synth.features(a.n, a.f, device=dev, seed=1)
     if rank == a.sb_oom_rank:
@@ -76,7 +83,19 @@ def main():
                                            p_drop=a.p_drop, seed=5, exchange=a.exchange)
     Z = runner.run()
     torch.cuda.synchronize()
-    if a.oracle:
+    if a.oracle_torch:
+        from oracle import ppnp_oracle as O
+
+        G = ppnp_amd.Graph.from_csr(indptr, indices, None, a.n, device=dev)
+        rp, col, val, _ = G.csr()
+        A = torch.sparse_csr_tensor(rp.cpu().long(), col.cpu().long(), val.cpu().double(),
+                                    size=(a.n, a.n))
+        G.close()
+        del rp, col, val
+        torch.set_num_threads(max(1, min(8, len(os.sched_getaffinity(0)))))
+        ref = O.appnp_propagate_torch_cpu(A, H.cpu().double(), a.K, a.alpha)
+        del A
+    elif a.oracle:
         import numpy as np
         import scipy.sparse as sp
 
@@ -91,7 +110,8 @@ def main():
         G = ppnp_amd.Graph.from_csr(indptr, indices, None, a.n, device=dev)
         ref = ppnp_amd.propagate_forward(G, H, a.K, a.alpha, p_drop=a.p_drop, seed=5)
     block = ref[runner.lo:runner.hi, runner.f_lo:runner.f_hi]
-    err = (Z.double() - block.double()).abs().max().item() if block.numel() else 0.0
+    got = Z if Z.device == block.device else Z.cpu()
+    err = (got.double() - block.double()).abs().max().item() if block.numel() else 0.0
     tol = 1e-5 * ref.abs().max().item() + 1e-6
     ok = err <= tol
     if a.expect_split is not None:
@@ -100,7 +120,8 @@ def main():
           f"overlap={runner.overlap} exchange={runner.exchange} split_cols={runner.remainder_cols} "
           f"rows [{runner.lo},{runner.hi}) "
           f"cols [{runner.f_lo},"
-          f"{runner.f_hi}) reference={'oracle' if a.oracle else 'hip'} max err {err:.3e} "
+          f"{runner.f_hi}) reference={'oracle' if a.oracle or a.oracle_torch else 'hip'} "
+          f"max err {err:.3e} "
           f"tol {tol:.3e} -> {'OK' if ok else 'FAIL'}",
           flush=True)
     flag = torch.tensor([0 if ok else 1], dtype=torch.int64,

@@ -94,7 +94,11 @@ def _free_port():
     (8, "4x2", True, "multipath", F),
     (4, "2x2", False, "multipath", F), (8, "2x4", True, "group", F),
     # column slabs cut at whole lines: 40 = 32 | 8, 100 = 32 | 32 | 36
-    (2, "col-lines", False, "group", 40), (3, "col-lines", False, "group", 100)])
+    (2, "col-lines", False, "group", 40), (3, "col-lines", False, "group", 100),
+    # uneven slabs on a 2-D layout: F = 73 on 2 x 2 is 37 | 36 columns, so the
+    # relayed exchange packs each origin's piece at its own column group's width
+    (4, "2x2", False, "multipath", 73), (4, "2x2", True, "multipath", 73),
+    (4, "2x2", True, "group", 73)])
 def test_partitioned_matches_oracle(world, layout, overlap, exchange, f):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -195,6 +199,16 @@ def test_layout_memory_and_index_limits():
     # a slab on the split-row path also holds the source-blocked copy of A_hat
     assert rank_bytes(Layout(1, 1), n, 100, nnz) - rank_bytes(Layout(1, 1), n, 96, nnz) >= 8 * nnz
     assert rank_bytes(Layout(1, 1), n, 100, nnz, elem_bytes=2) < rank_bytes(Layout(1, 1), n, 96, nnz)
+    # the line-cut column layout is held to its WIDEST slab (F = 200 on 2 ranks: 96 | 104 against
+    # the even 100 | 100): offered when that fits, dropped when only the even cut does
+    lines2 = (Layout(1, 2, True), False, "group")
+    assert lines2 in candidate_layouts(2, 200, n, nnz, 4, 288 * gb)
+    even, wide = rank_bytes(Layout(1, 2), n, 200, nnz), rank_bytes(Layout(1, 2), n, 200, nnz,
+                                                                   width=104)
+    assert wide > even
+    tight = int((even + wide) / 2 / 0.85)
+    assert choose_layout(2, n, 200, nnz, 4, tight) == Layout(1, 2)
+    assert lines2 not in candidate_layouts(2, 200, n, nnz, 4, tight)
 
 
 @pytest.mark.parametrize("spec,world", [("2x4", 8), ("4x2", 8), ("2x2", 4), ("2x3", 6)])
@@ -229,3 +243,37 @@ def test_multipath_plan(spec, world):
                 got[origin] += rows[1] - rows[0]
         group = MultipathComm(layout, r).group_of(r)
         assert dict(got) == {a: shard for a in group if a != r}
+
+
+def _agree_worker(rank, world, port, splits, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from ppnp_amd.dist import agree_split
+
+        q.put((rank, agree_split(splits[rank], "cpu")))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("splits,agreed", [
+    # every rank found the same split: kept
+    ([(32, 4)] * 4, (32, 4)),
+    # F = 73 on 2 x 2: column groups of 37 (32 + 5: a W8 copy) and 36 (32 + 4: W4) columns --
+    # the exchanged remainder parts would differ in width: whole rows everywhere
+    ([(32, 8), (32, 8), (32, 4), (32, 4)], None),
+    # different main widths (e.g. 68 | 36): whole rows
+    ([(64, 4), (64, 4), (32, 4), (32, 4)], None),
+    # one rank's best-effort copy failed: whole rows
+    ([(32, 4), None, (32, 4), (32, 4)], None)])
+def test_split_agreement_needs_equal_parts(splits, agreed):
+    """dist.agree_split, the collective decision of the row-group split layout: every rank
+    takes the split only if every rank found the same (main width, remainder width), since
+    the parts are exchanged between column groups as equal-size messages."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    mp.start_processes(_agree_worker, args=(4, _free_port(), splits, q), nprocs=4, join=True,
+                       start_method="spawn")
+    res = dict(q.get() for _ in range(4))
+    assert all(v == agreed for v in res.values()), res

@@ -385,6 +385,45 @@ def test_row_partition_split_rows_matches_oracle(ranks, extra):
     assert res == {r: "OK" for r in range(ranks)}, proc.stdout[-4000:]
 
 
+@pytest.mark.parametrize("extra", [["--overlap"], []])
+def test_products_row_partition_matches_oracle(extra):
+    """the north_star's row partition on config 5's own workload -- products-synth
+    (2,449,029 x 100, 126 M nonzeros) over 2 ranks sharing the GPU (gloo exchange), K = 2, every
+    rank on the split rows of its held rows (3 gathered lines + the L2-blocked remainder pass,
+    both parts exchanged), with and without the overlapped local/remote split.  Each rank's
+    block of Z_K against the float64 torch.sparse loop over the device A_hat, which
+    test_products_a_hat_matches_calc_a_hat pins to calc_a_hat (helpers.py:58-66)."""
+    env = dict(os.environ, PPNP_DIST_BACKEND="gloo", PYTHONPATH=ROOT, OMP_NUM_THREADS="8")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.join(ROOT, "tests", "dist_worker.py"), "--layout", "row", "--workload",
+           "products-synth", "--K", "2", "--oracle-torch", "--expect-split", "4", *extra]
+    proc = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=400)
+    assert proc.returncode == 0, proc.stdout[-3000:] + proc.stderr[-3000:]
+    res = _rank_results(proc.stdout, "dist_worker")
+    assert res == {0: "OK", 1: "OK"}, proc.stdout[-4000:]
+
+
+@pytest.mark.parametrize("f,exchange,split", [(72, "multipath", 4), (72, "group", 4),
+                                              (73, "multipath", 0)])
+def test_two_d_layout_split_rows_match_oracle(f, exchange, split):
+    """a 2 x 2 layout on 4 ranks sharing the GPU, on the split layout of its held rows.
+    F = 72 is 36 | 36 columns (32 + 4 on both column groups): the two parts of every iterate go
+    through the relayed exchange (MultipathComm) or the column-group all-gather.  F = 73 is
+    37 | 36 (a W8 copy beside a W4 copy): the ranks agree to keep whole rows instead of
+    exchanging parts of different widths.  Each rank's block against the float64 oracle."""
+    env = dict(os.environ, PPNP_DIST_BACKEND="gloo", PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=4",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.join(ROOT, "tests", "dist_worker.py"), "--layout", "2x2", "--f", str(f),
+           "--graph-n", "200000", "--graph-m", "1000000", "--K", "3", "--oracle", "--overlap",
+           "--exchange", exchange, "--expect-split", str(split)]
+    proc = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=200)
+    assert proc.returncode == 0, proc.stdout[-3000:] + proc.stderr[-3000:]
+    res = _rank_results(proc.stdout, "dist_worker")
+    assert res == {r: "OK" for r in range(4)}, proc.stdout[-4000:]
+
+
 def test_split_decision_is_collective():
     """The regrouped copy is best-effort: when it cannot be built on ONE rank (rank 1 here,
     APPNP_SB_TEST_OOM), every rank keeps whole rows -- both the Python row loop (an all-reduce at
