@@ -39,8 +39,6 @@ from __future__ import annotations
 
 import argparse
 import datetime
-import glob
-import hashlib
 import json
 import os
 import sys
@@ -136,13 +134,29 @@ def cpu_threads(world: int = 1) -> tuple[int, int]:
 
 
 def src_digest() -> str:
-    """Digest of the HIP sources: keys the committed PMC traffic to the kernels that made it."""
-    h = hashlib.sha1()
-    for p in sorted(glob.glob(os.path.join(ROOT, "ppnp_amd", "csrc", "*.hip"))
-                    + glob.glob(os.path.join(ROOT, "ppnp_amd", "csrc", "*.h"))):
-        with open(p, "rb") as fh:
-            h.update(os.path.basename(p).encode() + fh.read())
-    return h.hexdigest()[:12]
+    """Digest of the HIP sources (ppnp_amd/csrc/srcdigest.py, the same function the Makefile
+    compiles into the library): keys the committed PMC traffic to the kernels that made it."""
+    import importlib.util
+
+    path = os.path.join(ROOT, "ppnp_amd", "csrc", "srcdigest.py")
+    spec = importlib.util.spec_from_file_location("ppnp_srcdigest", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod.src_digest(os.path.dirname(path))
+
+
+def build_info() -> dict:
+    """Provenance of the library this process loaded: the source digest
+    compiled into it (appnp_build_info) against the digest of the sources in this tree.  A
+    library built from other sources reads ``match: false``."""
+    from ppnp_amd import _lib
+
+    lib = _lib.load()
+    info = lib.appnp_build_info().decode()
+    fields = dict(kv.split("=", 1) for kv in info.split(";") if "=" in kv)
+    here = src_digest()
+    return {"library": _lib.LIB_PATH, "info": info, "library_src": fields.get("src"),
+            "tree_src": here, "match": fields.get("src") == here}
 
 
 def traffic_key(workload, dtype_name, kernel_key, f_local, rows, overlap=False) -> str:
@@ -573,8 +587,11 @@ def main(argv=None):
         emu = dict(rank=r, world=P, comm=pdist.NullComm())
         lw = P
     esz = 2 if dtype == torch.bfloat16 else 4
-    mem = torch.cuda.get_device_properties(dev).total_memory
     nnz_bound = 2 * m + n  # nnz(A_hat) <= 2 m + n (symmetrised edges + diagonal)
+    # the device budget of a candidate: the GPU's memory less what this process holds beside
+    # it for the whole run -- the input CSR of A (int32) and H
+    held = 4 * (n + 1) + 4 * 2 * m + n * pdist.line_ld(F, esz) * esz
+    mem = torch.cuda.get_device_properties(dev).total_memory - held
     if args.layout == "auto" and world > 1 and not args.emulate:
         cands = pdist.candidate_layouts(world, F, n, nnz_bound, esz, mem)
     else:
@@ -620,6 +637,7 @@ def main(argv=None):
         adj_small = sp.csr_matrix((np.ones(len(ix_c), dtype=np.float32), ix_c, ip_c),
                                   shape=(n, n))
 
+    binfo = build_info()  # which library this process loaded, built from which sources
     extras = {}  # cpu_baseline, attached to whichever line is printed
     ORACLE_REF = "oracle fp32 torch.sparse.mm CPU loop (oracle/ppnp_oracle.py), same A_hat and H, "
 
@@ -684,6 +702,7 @@ def main(argv=None):
                 "parallelism": parallelism,
             },
             "roofline": rl,
+            "build": binfo,
         }
 
     stream = torch.cuda.current_stream(dev)

@@ -88,6 +88,11 @@ enum appnp_norm { APPNP_NORM_SYM = 0, APPNP_NORM_RW = 1 };
 enum appnp_dtype { APPNP_F32 = 0, APPNP_BF16 = 1 };
 
 int appnp_abi_version(void);
+/* Provenance of this build: "src=<digest of the .hip and .h files of ppnp_amd/csrc
+ * (srcdigest.py)>;abi=..;
+ * arch=gfx950;compiler=..;built=..".  bench.py prints it next to the digest of the tree it
+ * runs in, so a library built from other sources shows. */
+const char* appnp_build_info(void);
 const char* appnp_strerror(int code);
 
 /*

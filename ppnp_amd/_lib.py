@@ -35,6 +35,7 @@ _vp, _i64, _i32, _f32, _u64, _sz = C.c_void_p, C.c_int64, C.c_int, C.c_float, C.
 
 _SIGS = {
     "appnp_abi_version": (_i32, []),
+    "appnp_build_info": (C.c_char_p, []),
     "appnp_strerror": (C.c_char_p, [_i32]),
     "appnp_graph_create": (_i32, [_vp, _vp, _vp, _i64, _i64, _i32, _vp, C.POINTER(_vp)]),
     "appnp_graph_create_rows": (

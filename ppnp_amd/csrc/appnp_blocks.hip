@@ -68,7 +68,8 @@ namespace {
 
 constexpr int kRemThreads = kRemWaves * kWave;  // 1024 at 16 waves
 constexpr int kRemLdsBytes = 160 * 1024;        // LDS per CU on gfx950
-constexpr int kRemMaxRg = kRemLdsBytes / (kRemWaves * 16);  // 640 rows per wave group at 16
+// rows per wave group at 16 waves: 639 (LDS also holds the waves' progress counters, 64 B)
+constexpr int kRemMaxRg = (kRemLdsBytes - kRemWaves * 4) / (kRemWaves * 16);
 constexpr uint32_t kRemNone = 0xffffffffu;      // packed entry of an idle lane (row 4095)
 constexpr int kWalkWaves = kWavesPerBlock;      // build walk: one wave per group
 constexpr int kWalkMaxBlocks = 4096;            // LDS cursors of the build walk: 64 KiB
@@ -77,17 +78,13 @@ constexpr int kRemChunk = kWave;                // entries per chunk; segments p
 #define APPNP_REM_U 2
 #endif
 constexpr int kRemU = APPNP_REM_U;              // chunks in flight per wave (-DAPPNP_REM_U: measurement)
-// W8 / W16 passes (16 / 32 entries per chunk): 4 chunks in flight.  The 13-column slab of
-// products-synth (W16) took 1.93 ms at 4, 1.94 at 8, 2.01 at 2 and 2.25 at 1
-// (profiles/r4_w16_ab.txt)
-#ifndef APPNP_REM_U_WIDE
-#define APPNP_REM_U_WIDE 4
+// The W16 pass (16 entries per chunk) keeps 4 chunks in flight: the 13-column slab of
+// products-synth took 1.93 ms at 4, 1.94 at 8, 2.01 at 2 and 2.25 at 1; the W8 pass (F = 40)
+// 1.212 ms at 4 against 1.205 at 2 (profiles/r4_w16_ab.txt, r4_sync_ab.txt)
+#ifndef APPNP_REM_U_W16
+#define APPNP_REM_U_W16 4
 #endif
-constexpr int kRemUWide = APPNP_REM_U_WIDE;
-#ifndef APPNP_REM_SYNC_MASK
-#define APPNP_REM_SYNC_MASK 0
-#endif
-constexpr int kRemSyncMask = APPNP_REM_SYNC_MASK;
+constexpr int kRemUW16 = APPNP_REM_U_W16;
 
 static_assert(kRemMaxRg < (1 << kRemRowBits), "row in group must fit the packed entry");
 static_assert(kRemRowBits + kRemColBits == 32, "packed entry is 32 bits");
@@ -103,6 +100,9 @@ struct RemLayout {
                         // value
   int32_t nb, br_log2, slots, rg, passes;
   int32_t scale_out;    // VF: the output is the next remainder buffer (store dr o y)
+  int32_t sync;         // > 0: workgroup barrier after every `sync` source blocks (k_rem_persist)
+  int32_t window;       // > 0: a wave waits while it is more than `window` blocks ahead of the
+                        // slowest wave of its workgroup (k_rem_persist)
 };
 
 // ---- segmented inclusive scan over the 64 lanes (rows non-decreasing across lanes) --------
@@ -330,12 +330,14 @@ __device__ __forceinline__ void rem_walk(const StepArgs& a, const RemLayout& L,
 // VF (unit graph): entries carry no value -- the sum of the gathered dr_j Z_j is scaled by
 // dl_i in the epilogue, so the entry stream is 4 B per entry instead of 8 (0.91 -> 0.81 ms
 // per products-synth launch).
-// SYNC: the waves of a workgroup walk the source blocks in step, with a workgroup barrier after
-// every block.  Without it a wave streams its segments back to back, and the CU's oldest-first
-// arbitration spreads its waves over ~12 % of the sweep (profiles/r3_rem_timeline.txt): that
-// span of blocks must share the XCD's 4 MB L2, which a W4 table's 512-KB blocks do (92 % hits)
-// and a W16 table's 2-MB blocks do not (28 %; profiles/r4_w16_*).
-template <int EPI, int U, bool VF, int LPE, bool SYNC>
+// L.sync > 0: the waves of a workgroup walk the source blocks in step, with a workgroup barrier
+// after every L.sync blocks.  Without it a wave streams its segments back to back, and the
+// CU's oldest-first arbitration spreads its waves over ~12 % of the sweep
+// (profiles/r3_rem_timeline.txt): that span of blocks must share the XCD's 4 MB L2, which a W4
+// table's 512-KB blocks do (92 % hits) and a W16 table's 2-MB blocks do not (28 %;
+// profiles/r4_w16_ab.txt).  A barrier after every block lifts the W16 pass to 58 % hits but
+// costs more in waves idling at the barrier than the misses it saves (profiles/r4_sync_ab.txt).
+template <int EPI, int U, bool VF, int LPE>
 __global__ __launch_bounds__(kRemThreads) void k_rem_persist(StepArgs a, RemLayout L) {
   constexpr int CH = kWave / LPE;
   extern __shared__ f32x4 rem_acc[];
@@ -344,17 +346,42 @@ __global__ __launch_bounds__(kRemThreads) void k_rem_persist(StepArgs a, RemLayo
   f32x4* acc = rem_acc + (int64_t)wv * L.rg * LPE;
   const f32x4* __restrict__ z = static_cast<const f32x4*>(a.zin);
   const int64_t slot = (int64_t)blockIdx.x * kRemWaves + wv;
+  // blocks completed by each wave of the workgroup (window mode), after the accumulators
+  int* prog = reinterpret_cast<int*>(rem_acc + (int64_t)kRemWaves * L.rg * LPE);
+  if (L.window > 0) {
+    if (threadIdx.x < kRemWaves) prog[threadIdx.x] = 0;
+    __syncthreads();  // uniform: every wave takes this branch
+  }
   for (int p = 0; p < L.passes; ++p) {
     const int64_t g = (int64_t)p * L.slots + slot;
     const int64_t r0 = g * L.rg;
     const int rows = (int)max<int64_t>(0, min<int64_t>(L.rg, a.n_rows - r0));
     for (int r = lane; r < rows * LPE; r += kWave) acc[r] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    if constexpr (SYNC) {
-      // every wave runs the same nb blocks (an empty segment is 0 chunks), so every wave
-      // reaches every barrier
+    if (L.window > 0) {
+      // a wave more than `window` blocks ahead of the slowest wave of its workgroup yields
+      // (s_sleep) until that wave catches up: the waves of a CU stay within window + 1 blocks
+      // of each other without a barrier.  The slowest wave never waits, so all progress.
       for (int b = 0; b < L.nb; ++b) {
+        const int t = p * L.nb + b;
+        while (true) {
+          const int v = lane < kRemWaves
+                            ? __hip_atomic_load(prog + lane, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_WORKGROUP)
+                            : INT32_MAX;
+          if (!__ballot(v < t - L.window)) break;
+          __builtin_amdgcn_s_sleep(2);
+        }
         rem_walk<U, VF, LPE>(a, L, z, acc, r0, L.off[g * L.nb + b] / CH,
                              L.off[g * L.nb + b + 1] / CH);
+        if (lane == 0)
+          __hip_atomic_store(prog + wv, t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    } else if (L.sync > 0) {
+      // every wave runs the same nb blocks (an empty segment is 0 chunks) in the same steps,
+      // so every wave reaches every barrier; a wave's segments are contiguous in its stream
+      for (int b = 0; b < L.nb; b += L.sync) {
+        rem_walk<U, VF, LPE>(a, L, z, acc, r0, L.off[g * L.nb + b] / CH,
+                             L.off[g * L.nb + min(b + L.sync, L.nb)] / CH);
         __syncthreads();
       }
     } else {
@@ -506,43 +533,46 @@ __global__ __launch_bounds__(kBlock) void k_split_copy(const float* __restrict__
   }
 }
 
-template <int EPI, bool VF, int LPE, bool SYNC>
+template <int EPI, bool VF, int LPE>
 hipError_t launch_rem(dim3 grid, dim3 block, size_t lds, hipStream_t s, const StepArgs& a,
                       const RemLayout& L) {
-  constexpr int U = LPE == 1 ? kRemU : kRemUWide;
+  constexpr int U = LPE == 4 ? kRemUW16 : kRemU;
   static const hipError_t attr = hipFuncSetAttribute(  // > 64 KiB of dynamic LDS, once
-      reinterpret_cast<const void*>(k_rem_persist<EPI, U, VF, LPE, SYNC>),
+      reinterpret_cast<const void*>(k_rem_persist<EPI, U, VF, LPE>),
       hipFuncAttributeMaxDynamicSharedMemorySize, kRemLdsBytes);
   if (attr != hipSuccess) return attr;
-  hipLaunchKernelGGL((k_rem_persist<EPI, U, VF, LPE, SYNC>), grid, block, lds, s, a, L);
+  hipLaunchKernelGGL((k_rem_persist<EPI, U, VF, LPE>), grid, block, lds, s, a, L);
   return hipGetLastError();
-}
-
-int env_or(const char* name, int dflt);
-
-// Widths whose pass walks the source blocks in step (SYNC; bit LPE of the mask).
-// APPNP_REM_SYNC overrides the mask (measurement).
-int rem_sync_mask() {
-  static const int m = env_or("APPNP_REM_SYNC", kRemSyncMask);
-  return m;
 }
 
 template <int EPI, bool VF>
 hipError_t launch_rem_lpe(int lpe, dim3 grid, dim3 block, size_t lds, hipStream_t s,
                           const StepArgs& a, const RemLayout& L) {
-  const bool sync = (rem_sync_mask() >> lpe) & 1;
   switch (lpe) {
-    case 1:
-      return sync ? launch_rem<EPI, VF, 1, true>(grid, block, lds, s, a, L)
-                  : launch_rem<EPI, VF, 1, false>(grid, block, lds, s, a, L);
-    case 2:
-      return sync ? launch_rem<EPI, VF, 2, true>(grid, block, lds, s, a, L)
-                  : launch_rem<EPI, VF, 2, false>(grid, block, lds, s, a, L);
-    case 4:
-      return sync ? launch_rem<EPI, VF, 4, true>(grid, block, lds, s, a, L)
-                  : launch_rem<EPI, VF, 4, false>(grid, block, lds, s, a, L);
+    case 1: return launch_rem<EPI, VF, 1>(grid, block, lds, s, a, L);
+    case 2: return launch_rem<EPI, VF, 2>(grid, block, lds, s, a, L);
+    case 4: return launch_rem<EPI, VF, 4>(grid, block, lds, s, a, L);
     default: return hipErrorInvalidValue;
   }
+}
+
+int env_or(const char* name, int dflt);
+
+// Blocks between workgroup barriers of the pass of width 4 lpe (0: none, the default).
+// APPNP_REM_SYNC_W4 / _W8 / _W16 (measurement; profiles/r4_sync_ab.txt).
+int rem_sync_blocks(int lpe) {
+  static const int w4 = env_or("APPNP_REM_SYNC_W4", 0), w8 = env_or("APPNP_REM_SYNC_W8", 0),
+                   w16 = env_or("APPNP_REM_SYNC_W16", 0);
+  return lpe == 1 ? w4 : lpe == 2 ? w8 : w16;
+}
+
+// The progress window of the pass of width 4 lpe in blocks (0: free-running waves).
+// APPNP_REM_WINDOW_W4 / _W8 / _W16 (measurement).
+int rem_window_blocks(int lpe) {
+  static const int w4 = env_or("APPNP_REM_WINDOW_W4", 0),
+                   w8 = env_or("APPNP_REM_WINDOW_W8", 0),
+                   w16 = env_or("APPNP_REM_WINDOW_W16", 0);
+  return lpe == 1 ? w4 : lpe == 2 ? w8 : w16;
 }
 
 // fp32 copy of dinv (the unit graph's row / column scales)
@@ -726,10 +756,11 @@ hipError_t launch_remainder(const appnp_graph* g, const StepArgs& a_in, int epi,
   a.f = nv;
   if (a.n_rows <= 0) return hipSuccess;
   const bool vf = g->rb_val == nullptr;
-  RemLayout L{g->rb_off, g->rb_ent, g->rb_val, g->rb_cblk, g->rb_dl, g->rb_dr, g->rb_nb,
-              g->rb_br_log2, g->rb_slots, g->rb_rg, g->rb_passes, to_rem ? 1 : 0};
   const int lpe = g->rb_lpe;
-  const size_t lds = (size_t)kRemWaves * g->rb_rg * lpe * sizeof(f32x4);
+  RemLayout L{g->rb_off, g->rb_ent, g->rb_val, g->rb_cblk, g->rb_dl, g->rb_dr, g->rb_nb,
+              g->rb_br_log2, g->rb_slots, g->rb_rg, g->rb_passes, to_rem ? 1 : 0,
+              rem_sync_blocks(lpe), rem_window_blocks(lpe)};
+  const size_t lds = (size_t)kRemWaves * g->rb_rg * lpe * sizeof(f32x4) + kRemWaves * sizeof(int);
   const dim3 grid((unsigned)g->rb_grid), block(kRemThreads);
   if (epi == EPI_BWD)
     return vf ? launch_rem_lpe<EPI_BWD, true>(lpe, grid, block, lds, s, a, L)

@@ -236,6 +236,17 @@ extern "C" {
 
 int appnp_abi_version(void) { return PPNP_AMD_ABI_VERSION; }
 
+#ifndef APPNP_SRC_DIGEST
+#define APPNP_SRC_DIGEST "unknown"
+#endif
+#define APPNP_STR2(x) #x
+#define APPNP_STR(x) APPNP_STR2(x)
+
+const char* appnp_build_info(void) {
+  return "src=" APPNP_SRC_DIGEST ";abi=" APPNP_STR(PPNP_AMD_ABI_VERSION) ";arch=gfx950;compiler="
+      __VERSION__ ";built=" __DATE__ " " __TIME__;
+}
+
 const char* appnp_strerror(int code) {
   switch (code) {
     case APPNP_OK: return "ok";

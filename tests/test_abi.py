@@ -47,6 +47,35 @@ def test_abi_version_and_strerror():
     assert lib.appnp_strerror(_lib.APPNP_ENOTSUP) == b"not supported"
 
 
+def test_build_info_names_the_sources_of_this_tree():
+    """the library carries the digest of the HIP sources it was compiled from
+    (Makefile -> appnp_build_info), and it equals the digest of the sources in this tree
+    (ppnp_amd/csrc/srcdigest.py, what bench.py prints beside it).  A stale build fails here."""
+    import bench
+
+    info = bench.build_info()
+    assert info["info"].startswith("src=") and "arch=gfx950" in info["info"]
+    assert info["match"], info
+
+
+def test_line_rate_probe_validates_arguments():
+    """appnp_line_rate_probe returns before any launch on bad arguments (no device here)."""
+    from ppnp_amd import _lib
+
+    lib = _lib.load()
+    sink = C.c_void_p(0x1000)
+    assert lib.appnp_line_rate_probe(None, 1 << 20, 10, 0, sink, None) == _lib.APPNP_EINVAL
+    # a table base that is not 128-B aligned, a table under one line, a negative count
+    assert lib.appnp_line_rate_probe(C.c_void_p(0x1040), 1 << 20, 10, 0, sink,
+                                     None) == _lib.APPNP_EINVAL
+    assert lib.appnp_line_rate_probe(C.c_void_p(0x1000), 64, 10, 0, sink,
+                                     None) == _lib.APPNP_EINVAL
+    assert lib.appnp_line_rate_probe(C.c_void_p(0x1000), 1 << 20, -1, 0, sink,
+                                     None) == _lib.APPNP_EINVAL
+    assert lib.appnp_line_rate_probe(C.c_void_p(0x1000), 1 << 20, 0, 0, sink,
+                                     None) == _lib.APPNP_OK  # nothing to do
+
+
 def test_argument_validation_without_device():
     """Errors are returned as codes, never raised/aborted across the ABI."""
     from ppnp_amd import _lib

@@ -1,0 +1,13 @@
+#!/bin/bash
+# Build-container side of tools/profile_r4_pmc.sh: one profiles/r4p_<case>_summary.json (+ kernel
+# stats CSV) per case and its entry in profiles/pmc_traffic.json, keyed by the traffic_key its
+# bench line printed.
+set -eu
+cd "$(dirname "$0")/.."
+for d in gpurun_out/pmc/*/; do
+  tag=$(basename "$d")
+  [ -f "gpurun_out/${tag}_stats.log" ] || continue
+  python tools/summarize_profile.py "r4p_$tag" "$d/stats" "$d/fetch" "$d/write" \
+    --bench-json "gpurun_out/${tag}_stats.log" > /dev/null
+  echo "r4p_$tag"
+done

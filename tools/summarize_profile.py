@@ -43,16 +43,19 @@ def per_dispatch(path, match):
     return out, names
 
 
-def per_iteration(path, counter, kernels):
+def per_iteration(path, counter, kernels, iterations):
     """Counter total of one APPNP iteration: the sum over the dispatches of every kernel of
-    the iteration (the SpMM kernel first; with split rows also the remainder passes and the
-    per-call split copy) divided by the number of SpMM dispatches (one per iteration)."""
-    total, n_iter = 0.0, 0
-    for i, k in enumerate(kernels):
+    the iteration (the SpMM kernel; with split rows also the remainder passes and the per-call
+    split copy; with overlap the local and the remote launch) divided by the iterations the
+    profiled command ran ((warmup + steps) x K of its bench line).  Without a count, by the
+    dispatches of the first kernel that ran (one per iteration)."""
+    total, n_first = 0.0, 0
+    for k in kernels:
         d, _ = per_dispatch(path, k)
         total += sum(d[counter])
-        if i == 0:
-            n_iter = len(d[counter])
+        if not n_first:
+            n_first = len(d[counter])
+    n_iter = iterations or n_first
     return total / max(1, n_iter), n_iter
 
 
@@ -69,16 +72,27 @@ def main():
     a = p.parse_args()
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
+    bench = None
+    if a.bench_json:
+        for line in open(a.bench_json):
+            line = line.strip()
+            if line.startswith("{") and '"metric"' in line:
+                bench = json.loads(line)
+    # iterations of the profiled command: every propagation of its warm-up and timed steps
+    # (a --cpu-iters 0 run of one GPU or one emulated rank launches nothing else of these kernels)
+    iters = ((bench["warmup"] + bench["steps"]) * bench["config"]["K"]) if bench else 0
     stats = find(a.stats_dir, "kernel_stats.csv")
     shutil.copy(stats, os.path.join(prof, f"{a.tag}_kernel_stats.csv"))
     rows = list(csv.DictReader(open(stats)))
     kernels = a.kernels.split(",")
     kern = [r for r in rows if any(k in r["Name"] for k in kernels)]
-    spmm_calls = sum(int(r["Calls"]) for r in kern if kernels[0] in r["Name"])
+    first = next((k for k in kernels if any(k in r["Name"] for r in kern)), kernels[0])
+    spmm_calls = iters or sum(int(r["Calls"]) for r in kern if first in r["Name"])
     iter_ns = sum(float(r["TotalDurationNs"]) for r in kern) / max(1, spmm_calls)
     f_kib, n_iter = per_iteration(find(a.fetch_dir, "counter_collection.csv"), "FETCH_SIZE",
-                                  kernels)
-    w_kib, _ = per_iteration(find(a.write_dir, "counter_collection.csv"), "WRITE_SIZE", kernels)
+                                  kernels, iters)
+    w_kib, _ = per_iteration(find(a.write_dir, "counter_collection.csv"), "WRITE_SIZE", kernels,
+                             iters)
     fetch_b = 2.0 * f_kib * 1024
     write_b = w_kib * 1024
     summ = {
@@ -93,7 +107,7 @@ def main():
         "pmc": {
             "FETCH_SIZE_KiB_per_launch": f_kib,
             "WRITE_SIZE_KiB_per_launch": w_kib,
-            "per": "iteration (SpMM launch + remainder passes + split copy / K)",
+            "per": "iteration (SpMM launches + remainder pass + split copy / K)",
             "launches": n_iter,
             "fetch_bytes_corrected": fetch_b,
             "write_bytes": write_b,
@@ -102,11 +116,8 @@ def main():
                           "write = WRITE_SIZE KiB",
         },
     }
-    if a.bench_json:
-        for line in open(a.bench_json):
-            line = line.strip()
-            if line.startswith("{") and '"metric"' in line:
-                summ["bench"] = json.loads(line)
+    if bench:
+        summ["bench"] = bench
     if "bench" in summ:
         b = summ["bench"]
         # the bench's own key: workload, dtype, layout, the iteration's kernels and a digest of
