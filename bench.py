@@ -58,16 +58,18 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip-level param
 GATHER_LINE_CEILING = 60.0
 # xGMI: 7 links per GPU at 76.8 GB/s per direction (153.6 GB/s bidirectional)
 XGMI_IN_GBS = 7 * 76.8
-# The persistent remainder pass (appnp_blocks.hip), MEASURED: G nonzeros/s of one W-column pass
-# over products-synth's shape (127.3 M nonzeros, 2.45 M rows), its row passes included --
-# tools/blk_probe.hip, profiles/r2_blk_probe.txt: W4 0.680 ms (1 row pass), W8 1.165 ms (2),
-# W16 1.894 ms (4), the fastest block size of each; the arxiv shape (one row pass) is no faster
-# (139 / 96 / 65 G/s).  Its gathers are L2 requests and its cost is set by the L2 misses of
-# the block sweep and the row passes, so no byte peak prices it (VERDICT r3
-# weak #3: the 34.5 TB/s L2 byte peak put the 13-column slab's floor at 0.35 ms against the
-# probe's 1.89 ms).
-REM_PASS_RATE = {4: 187.4, 8: 109.3, 16: 67.3}
-REM_PASS_SOURCE = "tools/blk_probe.hip, profiles/r2_blk_probe.txt"
+# The persistent remainder pass (appnp_blocks.hip), MEASURED: the fastest G nonzeros/s of one
+# W-column pass over products-synth's shape (126-127 M nonzeros, 2.45 M rows), its row passes
+# and entry stream included.  W4: the probe, tools/blk_probe.hip 0.680 ms for 127.3 M
+# (profiles/r2_blk_probe.txt; the library's pass takes 0.766 ms).  W8 / W16: the library's own
+# pass since round 4's barrier every 32 blocks, faster than the round-2 probe (1.165 / 1.894 ms):
+# F = 40's W8 pass 1.105 ms and the 8-rank column slab's W16 pass 1.769 ms for 126.2 M
+# (profiles/r4_sync_ab.txt).  The arxiv shape (one row pass) is no faster.  Its gathers are L2
+# requests and its cost is set by the L2 misses of the block sweep and the row passes
+# (DESIGN.md 4.2, 9), so no byte peak prices it (the 34.5 TB/s L2 byte peak
+# put the 13-column slab's floor at 0.35 ms).
+REM_PASS_RATE = {4: 187.4, 8: 114.2, 16: 71.3}
+REM_PASS_SOURCE = "profiles/r2_blk_probe.txt (W4), profiles/r4_sync_ab.txt (W8, W16)"
 # The in-library line-rate probe run before the timed region (appnp_line_rate_probe): random
 # 128-B lines gathered from the bench's own H buffer, ~20 ms
 PROBE_LINES = 1 << 30

@@ -13,11 +13,13 @@
 //     [b * 2^15, (b+1) * 2^15), i.e. 512 KB of Z_rem, which sits in every XCD's 4 MB L2 while
 //     the chip gathers from it.  Every wave walks the blocks in the same order at about the
 //     same rate, so the blocks live in L2 at one time are the few between the slowest and
-//     the fastest wave.  Pacing measured slower every way it was tried: per-block counters
-//     with a workgroup barrier (8.33 against 8.15 ms per products-synth iteration), and
-//     per-wave signals with bounded waits inside groups of co-located workgroups, leading by
-//     1, 2 or 4 blocks (8.6 to 16.9 against 8.2 ms; tools/sweep_rem.sh, round-2 history).
-//     The gathers are close to the L2 request rate anyway: each is its own 16-B request.
+//     the fastest wave.  For this one-row-pass W4 pass, pacing measured slower every way it was
+//     tried: per-block counters with a workgroup barrier (8.33 against 8.15 ms per
+//     products-synth iteration), per-wave signals with bounded waits inside groups of
+//     co-located workgroups, leading by 1, 2 or 4 blocks (8.6 to 16.9 against 8.2 ms;
+//     round-2 history), an in-workgroup progress window, and barriers every 8-32 blocks
+//     (round 4, profiles/r4_sync_ab.txt).  The wider passes, whose 2-4 row passes let the
+//     waves drift much further, take a barrier every 32 blocks (k_rem_persist).
 //
 // The accumulators never leave the chip.  The launch is persistent -- one 1024-thread
 // workgroup per CU, each of its 16 waves owning a group of <= 640 destination rows whose
@@ -68,8 +70,7 @@ namespace {
 
 constexpr int kRemThreads = kRemWaves * kWave;  // 1024 at 16 waves
 constexpr int kRemLdsBytes = 160 * 1024;        // LDS per CU on gfx950
-// rows per wave group at 16 waves: 639 (LDS also holds the waves' progress counters, 64 B)
-constexpr int kRemMaxRg = (kRemLdsBytes - kRemWaves * 4) / (kRemWaves * 16);
+constexpr int kRemMaxRg = kRemLdsBytes / (kRemWaves * 16);  // 640 rows per wave group at 16
 constexpr uint32_t kRemNone = 0xffffffffu;      // packed entry of an idle lane (row 4095)
 constexpr int kWalkWaves = kWavesPerBlock;      // build walk: one wave per group
 constexpr int kWalkMaxBlocks = 4096;            // LDS cursors of the build walk: 64 KiB
@@ -101,8 +102,6 @@ struct RemLayout {
   int32_t nb, br_log2, slots, rg, passes;
   int32_t scale_out;    // VF: the output is the next remainder buffer (store dr o y)
   int32_t sync;         // > 0: workgroup barrier after every `sync` source blocks (k_rem_persist)
-  int32_t window;       // > 0: a wave waits while it is more than `window` blocks ahead of the
-                        // slowest wave of its workgroup (k_rem_persist)
 };
 
 // ---- segmented inclusive scan over the 64 lanes (rows non-decreasing across lanes) --------
@@ -330,13 +329,16 @@ __device__ __forceinline__ void rem_walk(const StepArgs& a, const RemLayout& L,
 // VF (unit graph): entries carry no value -- the sum of the gathered dr_j Z_j is scaled by
 // dl_i in the epilogue, so the entry stream is 4 B per entry instead of 8 (0.91 -> 0.81 ms
 // per products-synth launch).
-// L.sync > 0: the waves of a workgroup walk the source blocks in step, with a workgroup barrier
-// after every L.sync blocks.  Without it a wave streams its segments back to back, and the
-// CU's oldest-first arbitration spreads its waves over ~12 % of the sweep
-// (profiles/r3_rem_timeline.txt): that span of blocks must share the XCD's 4 MB L2, which a W4
-// table's 512-KB blocks do (92 % hits) and a W16 table's 2-MB blocks do not (28 %;
-// profiles/r4_w16_ab.txt).  A barrier after every block lifts the W16 pass to 58 % hits but
-// costs more in waves idling at the barrier than the misses it saves (profiles/r4_sync_ab.txt).
+// L.sync > 0 (the W8 / W16 passes, rem_sync_blocks): the waves of a workgroup walk the source
+// blocks in step, with a workgroup barrier after every L.sync blocks and at the end of every row
+// pass.  Without it a wave streams its segments back to back, and the CU's oldest-first
+// arbitration spreads its waves over ~12 % of a sweep (profiles/r3_rem_timeline.txt), and
+// further over the 2-4 row passes of a wide pass: the span of blocks in use must share the
+// XCD's 4 MB L2, which a W4 table's 512-KB blocks do (92 % hits) and a W16 table's 2-MB blocks
+// do not (28 %; profiles/r4_w16_ab.txt).  A barrier after every block lifts the W16 pass to
+// 58 % hits but leaves waves idle at every block; every 32 blocks keeps 52 % and wins
+// (profiles/r4_sync_ab.txt).  A softer per-block progress window (a wave ahead of its
+// workgroup's slowest by more than D blocks sleeps; LDS counters) lost at every width and D.
 template <int EPI, int U, bool VF, int LPE>
 __global__ __launch_bounds__(kRemThreads) void k_rem_persist(StepArgs a, RemLayout L) {
   constexpr int CH = kWave / LPE;
@@ -346,37 +348,12 @@ __global__ __launch_bounds__(kRemThreads) void k_rem_persist(StepArgs a, RemLayo
   f32x4* acc = rem_acc + (int64_t)wv * L.rg * LPE;
   const f32x4* __restrict__ z = static_cast<const f32x4*>(a.zin);
   const int64_t slot = (int64_t)blockIdx.x * kRemWaves + wv;
-  // blocks completed by each wave of the workgroup (window mode), after the accumulators
-  int* prog = reinterpret_cast<int*>(rem_acc + (int64_t)kRemWaves * L.rg * LPE);
-  if (L.window > 0) {
-    if (threadIdx.x < kRemWaves) prog[threadIdx.x] = 0;
-    __syncthreads();  // uniform: every wave takes this branch
-  }
   for (int p = 0; p < L.passes; ++p) {
     const int64_t g = (int64_t)p * L.slots + slot;
     const int64_t r0 = g * L.rg;
     const int rows = (int)max<int64_t>(0, min<int64_t>(L.rg, a.n_rows - r0));
     for (int r = lane; r < rows * LPE; r += kWave) acc[r] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    if (L.window > 0) {
-      // a wave more than `window` blocks ahead of the slowest wave of its workgroup yields
-      // (s_sleep) until that wave catches up: the waves of a CU stay within window + 1 blocks
-      // of each other without a barrier.  The slowest wave never waits, so all progress.
-      for (int b = 0; b < L.nb; ++b) {
-        const int t = p * L.nb + b;
-        while (true) {
-          const int v = lane < kRemWaves
-                            ? __hip_atomic_load(prog + lane, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_WORKGROUP)
-                            : INT32_MAX;
-          if (!__ballot(v < t - L.window)) break;
-          __builtin_amdgcn_s_sleep(2);
-        }
-        rem_walk<U, VF, LPE>(a, L, z, acc, r0, L.off[g * L.nb + b] / CH,
-                             L.off[g * L.nb + b + 1] / CH);
-        if (lane == 0)
-          __hip_atomic_store(prog + wv, t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-    } else if (L.sync > 0) {
+    if (L.sync > 0) {
       // every wave runs the same nb blocks (an empty segment is 0 chunks) in the same steps,
       // so every wave reaches every barrier; a wave's segments are contiguous in its stream
       for (int b = 0; b < L.nb; b += L.sync) {
@@ -558,22 +535,19 @@ hipError_t launch_rem_lpe(int lpe, dim3 grid, dim3 block, size_t lds, hipStream_
 
 int env_or(const char* name, int dflt);
 
-// Blocks between workgroup barriers of the pass of width 4 lpe (0: none, the default).
-// APPNP_REM_SYNC_W4 / _W8 / _W16 (measurement; profiles/r4_sync_ab.txt).
+// Source blocks between workgroup barriers of the pass of width 4 lpe (0: none).  The W8 and
+// W16 passes sweep the table in 2-4 row passes, and without barriers the CU's oldest-first
+// arbitration lets its fast waves run ahead across them; a barrier every 32 blocks (and so at
+// every row pass's end) re-aligns the waves: W16 1.94 -> 1.77 ms, W8 1.21 -> 1.10 ms on
+// products-synth, L2 hits 28 -> 52 % (W16).  Every block costs more at the barrier than the
+// misses save (2.26 ms), and the single-pass W4 pass gains nothing (0.766 against 0.769 ms);
+// profiles/r4_sync_ab.txt.  APPNP_REM_SYNC_W4 / _W8 / _W16 override (measurement).
 int rem_sync_blocks(int lpe) {
-  static const int w4 = env_or("APPNP_REM_SYNC_W4", 0), w8 = env_or("APPNP_REM_SYNC_W8", 0),
-                   w16 = env_or("APPNP_REM_SYNC_W16", 0);
+  static const int w4 = env_or("APPNP_REM_SYNC_W4", 0), w8 = env_or("APPNP_REM_SYNC_W8", 32),
+                   w16 = env_or("APPNP_REM_SYNC_W16", 32);
   return lpe == 1 ? w4 : lpe == 2 ? w8 : w16;
 }
 
-// The progress window of the pass of width 4 lpe in blocks (0: free-running waves).
-// APPNP_REM_WINDOW_W4 / _W8 / _W16 (measurement).
-int rem_window_blocks(int lpe) {
-  static const int w4 = env_or("APPNP_REM_WINDOW_W4", 0),
-                   w8 = env_or("APPNP_REM_WINDOW_W8", 0),
-                   w16 = env_or("APPNP_REM_WINDOW_W16", 0);
-  return lpe == 1 ? w4 : lpe == 2 ? w8 : w16;
-}
 
 // fp32 copy of dinv (the unit graph's row / column scales)
 __global__ __launch_bounds__(kBlock) void k_dinv_f32(const double* __restrict__ d, int64_t n,
@@ -759,8 +733,8 @@ hipError_t launch_remainder(const appnp_graph* g, const StepArgs& a_in, int epi,
   const int lpe = g->rb_lpe;
   RemLayout L{g->rb_off, g->rb_ent, g->rb_val, g->rb_cblk, g->rb_dl, g->rb_dr, g->rb_nb,
               g->rb_br_log2, g->rb_slots, g->rb_rg, g->rb_passes, to_rem ? 1 : 0,
-              rem_sync_blocks(lpe), rem_window_blocks(lpe)};
-  const size_t lds = (size_t)kRemWaves * g->rb_rg * lpe * sizeof(f32x4) + kRemWaves * sizeof(int);
+              rem_sync_blocks(lpe)};
+  const size_t lds = (size_t)kRemWaves * g->rb_rg * lpe * sizeof(f32x4);
   const dim3 grid((unsigned)g->rb_grid), block(kRemThreads);
   if (epi == EPI_BWD)
     return vf ? launch_rem_lpe<EPI_BWD, true>(lpe, grid, block, lds, s, a, L)

@@ -49,7 +49,7 @@ def test_narrow_column_slab_in_the_remainder_pass():
     """13 of 100 columns on 8 ranks: no direct gather (0 lines per nonzero), 4 L2 requests per
     nonzero in the W16 pass.  The ceiling prices the pass at its measured rate:
     at least 0.9x the probe's time for the slab's nonzeros, not the 0.35 ms the L2 byte peak
-    gave (ceiling.frac 0.51 against a measured 0.17)."""
+    gave (ceiling.frac 0.51 against a measured 0.09)."""
     rl = _check(bench.roofline(n=N, rows=N, nnz=NNZ, F_local=13, esz=4, avg_iter_ms=2.015,
                                fs=0, r=13, lpe=4), 2.015)
     assert rl["ceiling"]["lines_per_nonzero"] == 0
@@ -57,17 +57,22 @@ def test_narrow_column_slab_in_the_remainder_pass():
     assert rl["bytes_per_launch"] == 4 * (N + 1) + 8 * NNZ + 3 * N * 13 * 4
     c = rl["ceiling"]
     assert c["ms_per_iter"] >= 0.9 * W16_PROBE_MS * NNZ / W16_PROBE_NNZ
-    assert c["ms_per_iter"] >= c["hbm_ms"] and c["remainder_pass_rate_G_nnz_s"] == 67.3
+    assert c["ms_per_iter"] >= c["hbm_ms"] and c["remainder_pass_rate_G_nnz_s"] == 71.3
     assert rl["ceiling"]["frac"] < 0.2
 
 
-@pytest.mark.parametrize("lpe,probe_ms,passes", [(1, 0.680, 1), (2, 1.165, 2), (4, 1.894, 4)])
-def test_remainder_pass_priced_at_its_probe(lpe, probe_ms, passes):
-    """Every width of the pass: the ceiling's remainder term is the probe's own time for the
-    probe's nonzeros (profiles/r2_blk_probe.txt), within 1 %."""
-    rl = bench.roofline(n=N, rows=N, nnz=W16_PROBE_NNZ, F_local=4 * lpe, esz=4,
+@pytest.mark.parametrize("lpe,nnz,best_ms", [
+    (1, W16_PROBE_NNZ, 0.680),  # W4: the probe (profiles/r2_blk_probe.txt)
+    (2, NNZ, 1.105),            # W8: F = 40's pass with a barrier every 32 blocks (r4_sync_ab)
+    (4, NNZ, 1.769)])           # W16: the 13-column slab's pass, same (r4_sync_ab)
+def test_remainder_pass_priced_at_its_fastest_measurement(lpe, nnz, best_ms):
+    """Every width of the pass: the ceiling's remainder term is the fastest measured time of
+    that pass for the measured nonzeros, within 1 % -- never above what was measured, so the
+    ceiling stays a floor."""
+    rl = bench.roofline(n=N, rows=N, nnz=nnz, F_local=4 * lpe, esz=4,
                         avg_iter_ms=10.0, fs=0, r=4 * lpe, lpe=lpe)
-    assert rl["ceiling"]["remainder_pass_ms"] == pytest.approx(probe_ms, rel=0.01)
+    assert rl["ceiling"]["remainder_pass_ms"] == pytest.approx(best_ms, rel=0.01)
+    assert rl["ceiling"]["remainder_pass_ms"] <= best_ms * 1.001
 
 
 def test_row_layout_rank_with_exchange():
