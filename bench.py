@@ -153,10 +153,13 @@ def build_info() -> dict:
     library built from other sources reads ``match: false``."""
     from ppnp_amd import _lib
 
-    lib = _lib.load()
-    info = lib.appnp_build_info().decode()
-    fields = dict(kv.split("=", 1) for kv in info.split(";") if "=" in kv)
     here = src_digest()
+    try:
+        info = _lib.load().appnp_build_info().decode()
+    except Exception as e:  # noqa: BLE001 -- provenance is reported, never fatal to the line
+        return {"library": _lib.LIB_PATH, "info": f"{type(e).__name__}: {e}",
+                "library_src": None, "tree_src": here, "match": False}
+    fields = dict(kv.split("=", 1) for kv in info.split(";") if "=" in kv)
     return {"library": _lib.LIB_PATH, "info": info, "library_src": fields.get("src"),
             "tree_src": here, "match": fields.get("src") == here}
 
