@@ -26,12 +26,6 @@
 
 namespace appnp {
 
-// k_step_flat on by default (APPNP_FLAT overrides): see launch_step
-#ifndef APPNP_FLAT_DEFAULT
-#define APPNP_FLAT_DEFAULT 0
-#endif
-constexpr int kFlatDefault = APPNP_FLAT_DEFAULT;
-
 static int env_int(const char* name, int dflt) {
   const char* s = getenv(name);
   return (s && *s) ? atoi(s) : dflt;
@@ -273,123 +267,6 @@ __global__ __launch_bounds__(kBlock) void k_step_wide(StepArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------
-// flat: one wavefront per row whose fp32 row of PC 16-B pieces leaves lanes of a power-of-two
-// group idle (PC = 24: the 96 main columns of a split F = 100 row, 3 lines, on G = 32 lanes of
-// which 24 work).  Every lane takes a piece of SOME entry instead: in a group of J = PC /
-// gcd(64, PC) wave instructions the 64 J lanes cover E = 64 J / PC whole entries, lane l of
-// instruction j taking piece (64 j + l) % PC of entry (64 j + l) / PC.  Each instruction then
-// carries 64 16-B pieces (8 whole lines at PC = 24) instead of 2 x 24, and a lane keeps one
-// accumulator per instruction of the group, whose piece never changes.  At the row's end the
-// E partials of each piece are summed through LDS in a fixed order (bitwise deterministic).
-// ------------------------------------------------------------------------------------------
-constexpr int gcd_c(int x, int y) { return y == 0 ? x : gcd_c(y, x % y); }
-
-template <int PC, int EPI, int U>
-__device__ __forceinline__ void wave_row_flat(const StepArgs& a, int64_t row, int lane, int2* tile,
-                                              f32x4* red) {
-  constexpr int J = PC / gcd_c(kWave, PC);  // instructions per group
-  constexpr int E = kWave * J / PC;         // entries per group
-  const float* __restrict__ zin = static_cast<const float*>(a.zin);
-  int eo[J], qo[J];
-#pragma unroll
-  for (int j = 0; j < J; ++j) {
-    eo[j] = (kWave * j + lane) / PC;
-    qo[j] = (kWave * j + lane) % PC;
-  }
-  const int beg = a.row_ptr[row];
-  const int end = a.row_ptr[row + 1];
-  float hv[4];
-  if (lane < PC) load_h<float, 4, EPI, false>(a, row, 4 * lane, hv, 4);
-  f32x4 acc[J];
-#pragma unroll
-  for (int j = 0; j < J; ++j) acc[j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-
-  for (int cb = beg; cb < end; cb += kWave) {
-    const int n = min(kWave, end - cb);
-    int c = 0;
-    float w = 0.0f;
-    if (lane < n) {
-      float v = 1.0f;
-      if (a.nt & 1) {
-        c = ld_nt<int32_t>(a.col + cb + lane);
-        if (a.val) v = ld_nt<float>(a.val + cb + lane);
-      } else {
-        c = a.col[cb + lane];
-        if (a.val) v = a.val[cb + lane];
-      }
-      w = edge_weight(v, a.row_lo + row, c, a);
-    }
-    tile[lane] = make_int2(c, __float_as_int(w));
-    __builtin_amdgcn_wave_barrier();
-    for (int g0 = 0; g0 < n; g0 += E * U) {
-      f32x4 z[U][J];
-      float wt[U][J];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-#pragma unroll
-        for (int j = 0; j < J; ++j) {
-          const int e = g0 + u * E + eo[j];
-          z[u][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-          wt[u][j] = 0.0f;
-          if (e < n) {
-            const int2 t = tile[e];
-            wt[u][j] = __int_as_float(t.y);
-            z[u][j] = *reinterpret_cast<const f32x4*>(zin + (int64_t)t.x * a.ld_in + 4 * qo[j]);
-          }
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-#pragma unroll
-        for (int j = 0; j < J; ++j) {
-          acc[j].x = fmaf(wt[u][j], z[u][j].x, acc[j].x);
-          acc[j].y = fmaf(wt[u][j], z[u][j].y, acc[j].y);
-          acc[j].z = fmaf(wt[u][j], z[u][j].z, acc[j].z);
-          acc[j].w = fmaf(wt[u][j], z[u][j].w, acc[j].w);
-        }
-      }
-    }
-    __builtin_amdgcn_wave_barrier();
-  }
-  // the partial of piece q sits at red[q + PC k], k = 0..E-1: fixed-order sum
-#pragma unroll
-  for (int j = 0; j < J; ++j) red[kWave * j + lane] = acc[j];
-  __builtin_amdgcn_wave_barrier();
-  if (lane < PC) {
-    f32x4 s = red[lane];
-#pragma unroll
-    for (int k = 1; k < E; ++k) {
-      const f32x4 r = red[lane + PC * k];
-      s = f32x4{s.x + r.x, s.y + r.y, s.z + r.z, s.w + r.w};
-    }
-    const float sv[4] = {s.x, s.y, s.z, s.w};
-    epilogue<float, 4, EPI, false>(a, row, 4 * lane, sv, hv, 4);
-  }
-  __builtin_amdgcn_wave_barrier();
-}
-
-template <int PC, int EPI, int U>
-__global__ __launch_bounds__(kBlock) void k_step_flat(StepArgs a) {
-  constexpr int J = PC / gcd_c(kWave, PC);
-  __shared__ int2 stage[kWavesPerBlock][kWave];
-  __shared__ f32x4 red[kWavesPerBlock][kWave * J];
-  const int lane = threadIdx.x & (kWave - 1);
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t nwaves = (int64_t)gridDim.x * kWavesPerBlock;
-  const int64_t total = a.n_rows + a.n_hub;  // hub rows first, as k_step_wide
-  for (int64_t v = (int64_t)blockIdx.x * kWavesPerBlock + wave; v < total; v += nwaves) {
-    int64_t row;
-    if (v < a.n_hub) {
-      row = a.hub[v];
-    } else {
-      row = v - a.n_hub;
-      if (a.hub && a.row_ptr[row + 1] - a.row_ptr[row] > kHubRow) continue;
-    }
-    wave_row_flat<PC, EPI, U>(a, row, lane, stage[wave], red[wave]);
-  }
-}
-
-// ------------------------------------------------------------------------------------------
 // narrow: one G-lane group per row, P = 64/G rows per wave.  Rows longer than a.heavy_thr
 // (listed in a.heavy at graph creation) are skipped here and processed by the trailing
 // blocks (blockIdx.x >= a.light_blocks), one whole wavefront per row (wave_row), so a hub row
@@ -534,22 +411,6 @@ hipError_t launch_v(int V, int G, bool wide, int uw, int un, dim3 grid, const St
   }
 }
 
-template <int EPI, int U>
-hipError_t launch_flat_pc(int pc, dim3 grid, const StepArgs& a, hipStream_t s) {
-  const dim3 block(kBlock);
-  switch (pc) {
-    case 12: hipLaunchKernelGGL((k_step_flat<12, EPI, U>), grid, block, 0, s, a); break;
-    case 24: hipLaunchKernelGGL((k_step_flat<24, EPI, U>), grid, block, 0, s, a); break;
-    default: return hipErrorNotSupported;
-  }
-  return hipGetLastError();
-}
-
-template <int EPI>
-hipError_t launch_flat(int pc, int u, dim3 grid, const StepArgs& a, hipStream_t s) {
-  return u >= 2 ? launch_flat_pc<EPI, 2>(pc, grid, a, s) : launch_flat_pc<EPI, 1>(pc, grid, a, s);
-}
-
 }  // namespace
 
 // Largest vector width (elements) valid for every operand: all leading dims and all base
@@ -646,22 +507,6 @@ hipError_t launch_step(int dtype, int epi, int V, const StepArgs& a_in, hipStrea
   const int un = un_env > 0 ? un_env : latency ? 8 : 4;
   static const int nt_env = env_int("APPNP_NT", -1);
   a.nt = nt_env >= 0 ? nt_env : (latency ? 0 : 1);
-  // fp32 rows of PC = 12 or 24 16-B pieces whose lane group would leave lanes idle (F = 48, 96:
-  // the 96 main columns of a split F = 100 row): the flat mapping, every lane of an instruction
-  // on a piece (k_step_flat).  APPNP_FLAT=0/1 and APPNP_FLAT_U (groups in flight) override.
-  static const int flat_env = env_int("APPNP_FLAT", kFlatDefault);
-  static const int flat_u = env_int("APPNP_FLAT_U", 1);
-  if (flat_env > 0 && dtype == 0 && wide && V == 4 && slabs == 1 && a.f % 4 == 0 &&
-      (int64_t)G * 4 > a.f && !latency) {
-    hipError_t r = hipErrorNotSupported;
-    switch (epi) {
-      case EPI_FWD: r = launch_flat<EPI_FWD>((int)(a.f / 4), flat_u, grid, a, s); break;
-      case EPI_BWD: r = launch_flat<EPI_BWD>((int)(a.f / 4), flat_u, grid, a, s); break;
-      case EPI_PARTIAL: r = launch_flat<EPI_PARTIAL>((int)(a.f / 4), flat_u, grid, a, s); break;
-      case EPI_FINISH: r = launch_flat<EPI_FINISH>((int)(a.f / 4), flat_u, grid, a, s); break;
-    }
-    if (r != hipErrorNotSupported) return r;
-  }
   if (dtype == 0) {
     switch (epi) {
       case EPI_FWD: return launch_v<float, EPI_FWD>(V, G, wide, uw, un, grid, a, s);
