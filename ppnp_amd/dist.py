@@ -901,40 +901,52 @@ def candidate_layouts(world: int, f: int, n: int = 0, nnz_hat: int = 0, elem_byt
                       mem_bytes: int | None = None):
     """(layout, overlap, exchange) variants ``bench.py --layout auto`` measures, the fastest of
     which it reports (max over ranks).  The first is ``choose_layout``'s: the column partition,
-    which needs no exchange, whenever it fits.  From 4 ranks on, the two 2-D layouts with 2 row
-    groups or 2 column groups -- 2 x (P/2) (half of each rank's gathers for half a slab of
-    exchange) and (P/2) x 2 (a quarter of the rows on 8 ranks, two-line gathers) -- each with the
-    relayed and the group exchange, which only an xGMI measurement can price (DESIGN.md section
-    5).  Then the north_star's pure row partition (overlapped all-gather, and the library's own
-    loop).  Candidates that do not fit (``fits``) are dropped; if none does, the row-heaviest
-    layout that fits is used."""
+    which needs no exchange, whenever it fits (and its cut at whole lines where that differs).
+    Then the north_star's pure row partition (overlapped all-gather) and, from 4 ranks on, the
+    two 2-D layouts with 2 row groups or 2 column groups -- 2 x (P/2) (half of each rank's
+    gathers for half a slab of exchange) and (P/2) x 2 (a quarter of the rows on 8 ranks,
+    two-line gathers) -- which only an xGMI measurement can price.
+
+    Order (round 4): by how standard the exchange is, since a candidate that stalls ends the
+    run at its deadline with the best line so far (bench.run_candidates), so whatever comes
+    after it is never measured: exchange-free layouts; the row partition's all-gather over all
+    ranks; the 2-D layouts' all-gathers within column groups; the library's own row loop
+    (RCCL called from C); last the relayed exchange (batched RCCL send/recv).  Candidates that
+    do not fit (``fits``) are dropped; if none does, the row-heaviest layout that fits is used."""
     first = choose_layout(world, n, f, nnz_hat, elem_bytes, mem_bytes)
     row = Layout(world, 1)
     # the north_star's design -- a pure row partition, all-gather overlapped with the local
     # product -- is always timed when it fits, so the scaling run measures it next to the rest
-    row_cand = ([(row, True, "group"), (row, True, "native")]
-                if world >= 2 and fits(row, n, f, nnz_hat, elem_bytes, True, mem_bytes) else [])
+    row_fits = world >= 2 and fits(row, n, f, nnz_hat, elem_bytes, True, mem_bytes)
+    two_d = []
     if first.rows > 1:  # row groups forced by size: overlap the exchange, try both routes
-        cands = ([(first, True, "multipath"), (first, True, "group")] if first.cols > 1 else
-                 [(first, True, "group")])
-        return cands + [c for c in row_cand if c[0] != first]
-    cands = [(first, False, "group")]
-    # the column layout cut at whole lines (exchange-free too): fewer lines per gather on the
-    # ranks that get whole lines, when that differs from the even cut
-    lines = line_slab_cols(f, world, elem_bytes) if first == Layout(1, world) else None
-    if (lines and lines != [col_range(f, world, c) for c in range(world)]
-            and fits(Layout(1, world, True), n, f, nnz_hat, elem_bytes, False, mem_bytes,
-                     width=max(hi - lo for lo, hi in lines))):
-        cands.append((Layout(1, world, True), False, "group"))
-    if world >= 4 and world % 2 == 0:
-        seen = {first}
-        for lay in (Layout(2, world // 2), Layout(world // 2, 2)):
-            if lay in seen or lay.rows == world or f < lay.cols:
-                continue
-            seen.add(lay)
-            if fits(lay, n, f, nnz_hat, elem_bytes, True, mem_bytes):
-                cands += [(lay, True, "multipath"), (lay, True, "group")]
-    return cands + [c for c in row_cand if c[0] != first]
+        if first.cols > 1:
+            two_d.append(first)
+        cands = [(first, True, "group")]
+    else:
+        cands = [(first, False, "group")]
+        # the column layout cut at whole lines (exchange-free too): fewer lines per gather on
+        # the ranks that get whole lines, when that differs from the even cut
+        lines = line_slab_cols(f, world, elem_bytes) if first == Layout(1, world) else None
+        if (lines and lines != [col_range(f, world, c) for c in range(world)]
+                and fits(Layout(1, world, True), n, f, nnz_hat, elem_bytes, False, mem_bytes,
+                         width=max(hi - lo for lo, hi in lines))):
+            cands.append((Layout(1, world, True), False, "group"))
+        if world >= 4 and world % 2 == 0:
+            seen = {first}
+            for lay in (Layout(2, world // 2), Layout(world // 2, 2)):
+                if lay in seen or lay.rows == world or f < lay.cols:
+                    continue
+                seen.add(lay)
+                if fits(lay, n, f, nnz_hat, elem_bytes, True, mem_bytes):
+                    two_d.append(lay)
+    if row_fits and row != first:
+        cands.append((row, True, "group"))
+    cands += [(lay, True, "group") for lay in two_d if lay != first]
+    if row_fits:
+        cands.append((row, True, "native"))
+    cands += [(lay, True, "multipath") for lay in two_d]
+    return cands
 
 
 def choose_layout(world: int, n: int, f: int, nnz: int, elem_bytes: int = 4,
