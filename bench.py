@@ -765,8 +765,8 @@ def main(argv=None):
         torch.distributed.broadcast(have, 0, group=ctl)
         use_oracle = bool(have.item())
         if use_oracle:
-            if rank != 0:
-                Zc = torch.empty(n, F, dtype=torch.float32)
+            Zc = (Zc.float().contiguous() if rank == 0
+                  else torch.empty(n, F, dtype=torch.float32))
             torch.distributed.broadcast(Zc, 0, group=ctl)
     use_oracle = use_oracle and Zc is not None
     Zref = None
