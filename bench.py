@@ -70,6 +70,11 @@ XGMI_IN_GBS = 7 * 76.8
 # put the 13-column slab's floor at 0.35 ms).
 REM_PASS_RATE = {4: 187.4, 8: 114.2, 16: 71.3}
 REM_PASS_SOURCE = "profiles/r2_blk_probe.txt (W4), profiles/r4_sync_ab.txt (W8, W16)"
+# N > 1: the whole run's wall budget, below the driver's 600 s bench timeout with
+# room for the launcher, the first `import torch` of a fresh box and the teardown; a candidate
+# is not started with less than MIN_CANDIDATE_S of it left
+RUN_BUDGET_S = 420.0
+MIN_CANDIDATE_S = 20.0
 # The in-library line-rate probe run before the timed region (appnp_line_rate_probe): random
 # 128-B lines gathered from the bench's own H buffer, ~20 ms
 PROBE_LINES = 1 << 30
@@ -104,6 +109,12 @@ def parse(argv=None):
     p.add_argument("--candidate-timeout", type=float, default=240.0,
                    help="N > 1: seconds one layout candidate (build, warm-up, timed steps, "
                         "parity) may take before the run is ended with the best line so far")
+    p.add_argument("--run-budget", type=float, default=RUN_BUDGET_S,
+                   help="N > 1: wall seconds, counted from this process's start, after which no "
+                        "further candidate starts and a running one is cut short (its deadline "
+                        "is the smaller of --candidate-timeout and the budget left); the best "
+                        "line so far is printed.  Keep it below the driver's bench timeout "
+                        "(600 s); 0 disables it")
     return p.parse_args(argv)
 
 
@@ -407,6 +418,44 @@ def time_steps(run, stream, steps, warmup, world, ctl):
     return wall, dev_ms, steps_ms
 
 
+def kernel_split(run, device, K, iteration_ms):
+    """roofline.kernel_ms: the device time of every launch of ONE untimed propagation, run right
+    after the timed region with the library's per-launch timer (appnp_kernel_timer_*: a HIP event
+    on the launch stream after each launch; no profiler, which changed the timing state in round
+    3), summarised per kind and per iteration beside the timed region's own iteration time
+    (VERDICT r4 #1).  ``sum_of_kernels`` below ``iteration`` means the timed launches ran faster
+    than the instrumented ones; above it, that they overlapped without the events between them."""
+    from ppnp_amd.ops import kernel_times
+
+    try:
+        torch.cuda.synchronize(device)
+        t = kernel_times(run, device)
+    except Exception as e:  # noqa: BLE001 -- a diagnostic, not the measurement
+        log(f"[bench] kernel split failed: {type(e).__name__}: {e}")
+        return None
+    by = {}
+    for kind, ms in t:
+        by.setdefault(kind, []).append(ms)
+
+    def stats(v):
+        return ({"mean": sum(v) / len(v), "min": min(v), "max": max(v), "launches": len(v)}
+                if v else None)
+
+    total = sum(ms for _, ms in t)
+    return {
+        "main": stats(by.get("step", [])),
+        "rem": stats(by.get("rem", [])),
+        "copy": stats(by.get("copy", [])),
+        "sum_of_kernels": total / K if K else total,
+        "iteration": iteration_ms,
+        "launches": [kind for kind, _ in t],
+        "source": "appnp_kernel_timer_begin/_end (include/ppnp_amd.h): one untimed propagation "
+                  "after the timed region, a HIP event after every launch on its stream; "
+                  "main = the SpMM kernel, rem = the remainder pass, copy = the split copy "
+                  "(once per call); sum_of_kernels and iteration are ms per iteration",
+    }
+
+
 class Deadline:
     """Wall-clock deadline of one layout candidate.  If it expires, ``on_expire`` runs on the
     timer thread (it never returns: it ends the process).  ``finish`` disarms it; the lock makes
@@ -445,8 +494,23 @@ def _abort_rccl():
         log(f"[bench] process-group abort: {type(e).__name__}: {e}")
 
 
+def process_age_s() -> float:
+    """Seconds since this process started (the run budget's clock): the kernel's start time of
+    the process, so the first ``import torch`` of a fresh box (1-2 minutes) counts too."""
+    try:
+        import psutil
+
+        return max(0.0, time.time() - psutil.Process().create_time())
+    except Exception:  # noqa: BLE001 -- psutil missing: count from this module's import
+        return time.monotonic() - _T_IMPORT
+
+
+_T_IMPORT = time.monotonic()
+
+
 def run_candidates(cands, measure, ctl, timeout_s, emit, name_of, rank, world,
-                   abort=_abort_rccl, exit_fn=os._exit, exchanges=lambda cand: False):
+                   abort=_abort_rccl, exit_fn=os._exit, exchanges=lambda cand: False,
+                   budget_s=0.0, age=process_age_s):
     """Measure every candidate in order and return (best result, {name: ms per step or None}).
 
     ``measure(cand)`` builds the candidate, times it (``time_steps``), checks parity and returns
@@ -457,15 +521,35 @@ def run_candidates(cands, measure, ctl, timeout_s, emit, name_of, rank, world,
     result so far (autotune marked "timeout") and the process ends through ``exit_fn`` -- the
     same on every rank, whose deadlines expire together.  The first candidate is normally the
     layout without a data-path exchange, which needs no deadline; one that ``exchanges`` (row
-    groups forced by memory: it brings RCCL up) gets one too."""
+    groups forced by memory: it brings RCCL up) gets one too.
+
+    ``budget_s`` > 0 bounds the whole run: before every candidate after the
+    first, the ranks agree on the largest ``age()`` (seconds since process start) over the
+    control group; with less than MIN_CANDIDATE_S of the budget left, this and every later
+    candidate are recorded as "skipped: run budget" and the best line so far is returned;
+    otherwise the candidate's deadline is the smaller of ``timeout_s`` and the budget left."""
     best, times = None, {}
     for i, cand in enumerate(cands):
         name = name_of(cand)
+        cand_timeout = timeout_s
+        if budget_s > 0 and i > 0:
+            t = torch.tensor([age()], dtype=torch.float64)
+            if world > 1:
+                torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX, group=ctl)
+            left = budget_s - float(t[0])
+            if left < MIN_CANDIDATE_S:
+                for rest in cands[i:]:
+                    times[name_of(rest)] = "skipped: run budget"
+                if rank == 0:
+                    log(f"[bench] run budget of {budget_s:.0f} s nearly spent ({left:.0f} s "
+                        f"left): skipping {len(cands) - i} candidate(s)")
+                break
+            cand_timeout = min(timeout_s, left) if timeout_s > 0 else left
         if rank == 0:
             log(f"[bench] candidate {name}: building and timing")
 
-        def expire(name=name):
-            log(f"[bench] candidate {name} passed its {timeout_s:.0f} s deadline on rank "
+        def expire(name=name, cand_timeout=cand_timeout):
+            log(f"[bench] candidate {name} passed its {cand_timeout:.0f} s deadline on rank "
                 f"{rank}: aborting the exchange, keeping the best line so far")
             t = threading.Thread(target=abort, daemon=True)
             t.start()
@@ -477,8 +561,8 @@ def run_candidates(cands, measure, ctl, timeout_s, emit, name_of, rank, world,
             exit_fn(0 if best is not None else 3)
 
         res, err = None, ""
-        guard = (Deadline(timeout_s, expire)
-                 if timeout_s > 0 and (i > 0 or exchanges(cand)) else None)
+        guard = (Deadline(cand_timeout, expire)
+                 if cand_timeout > 0 and (i > 0 or exchanges(cand)) else None)
         if guard:
             guard.__enter__()
         try:
@@ -674,6 +758,7 @@ def main(argv=None):
                       exchange_in_bytes=exchange_in, kernel=desc, kernel_key=kkey,
                       traffic=committed_traffic(tkey))
         rl["traffic_key"] = tkey
+        rl["kernel_ms"] = kernel_split(runner.run, dev, K, avg_iter_ms)
         rl["box_line_rate"] = box["G_lines_s"] if box else None
         rl["box_line_probe"] = (dict(box, source="appnp_line_rate_probe (ppnp_amd/csrc/"
                                      "appnp_probe.hip): random 128-B lines of the H buffer, "
@@ -836,7 +921,8 @@ def main(argv=None):
             res["config"]["autotune_ms_per_step"] = {cand_name(cands[0]): res["ms_per_step"]}
     else:
         res, _ = run_candidates(cands, measure, ctl, args.candidate_timeout, emit, cand_name,
-                                rank, world, exchanges=lambda c: c[0].rows > 1)
+                                rank, world, exchanges=lambda c: c[0].rows > 1,
+                                budget_s=args.run_budget if world > 1 else 0.0)
     if rank == 0:
         emit(res)
     if world > 1:

@@ -383,6 +383,28 @@ int appnp_allgather_rccl(void* buf, size_t shard_bytes, int rank, int nranks, vo
 int appnp_line_rate_probe(const void* table, int64_t table_bytes, int64_t lines, uint64_t seed,
                           float* sink, void* stream);
 
+/*
+ * Measurement aid (no counterpart in the reference): the device time of every launch of the
+ * calls made between appnp_kernel_timer_begin and appnp_kernel_timer_end on the calling thread.
+ * begin records a start event on `stream`; while the timer is on, appnp_propagate,
+ * appnp_propagate_bwd, appnp_step, appnp_step_split and appnp_split_copy (and so
+ * appnp_dist_propagate) record a timing event after each launch, tagged with its kind.  The
+ * events sit between launches that are stream-ordered anyway, so the launches run as they
+ * would without them, but a call timed this way is not graph-capturable.  end waits for the
+ * events and writes, for the first min(n, max) launches, kinds[i] (APPNP_KT_*) and ms[i]: the
+ * time from the previous event on the same stream (the start event, or the previous launch) to
+ * this launch's end, NaN if there is none.  *n_out = launches recorded; APPNP_ERANGE if more
+ * than max_launches were enqueued (the rest were not timed).  bench.py prints the split of one
+ * propagation as roofline.kernel_ms.
+ */
+enum appnp_kernel_kind {
+  APPNP_KT_COPY = 1,  /* H (or dZ) into the split layout, or a plain copy / scale of rows */
+  APPNP_KT_STEP = 2,  /* the fused SpMM + AXPBY kernel (whole rows or the main columns)  */
+  APPNP_KT_REM = 3    /* the persistent L2-blocked remainder pass                         */
+};
+int appnp_kernel_timer_begin(int max_launches, void* stream);
+int appnp_kernel_timer_end(float* ms, int* kinds, int max, int* n_out);
+
 #ifdef __cplusplus
 }
 #endif

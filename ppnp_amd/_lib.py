@@ -30,6 +30,7 @@ GRAPH_SB_W8 = 0x400  # remainder of up to 8 columns (include/ppnp_amd.h)
 GRAPH_SB_W16 = 0x800  # up to 16
 F32, BF16 = 0, 1
 PART_ALL, PART_LOCAL, PART_REMOTE = 0, 1, 2
+KT_COPY, KT_STEP, KT_REM = 1, 2, 3  # appnp_kernel_kind
 
 _vp, _i64, _i32, _f32, _u64, _sz = C.c_void_p, C.c_int64, C.c_int, C.c_float, C.c_uint64, C.c_size_t
 
@@ -97,6 +98,8 @@ _SIGS = {
     "appnp_dist_destroy": (None, [_vp]),
     "appnp_allgather_rccl": (_i32, [_vp, _sz, _i32, _i32, _vp, _vp]),
     "appnp_line_rate_probe": (_i32, [_vp, _i64, _i64, _u64, _vp, _vp]),
+    "appnp_kernel_timer_begin": (_i32, [_i32, _vp]),
+    "appnp_kernel_timer_end": (_i32, [_vp, _vp, _i32, C.POINTER(_i32)]),
     "appnp_step": (
         _i32,
         [_vp, _i32, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _f32,

@@ -4,15 +4,58 @@
 // synchronisation or allocation happens in appnp_propagate / appnp_propagate_bwd /
 // appnp_step, so a caller may capture them in a hipGraph.
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <new>
+#include <vector>
 
 #include "../../include/ppnp_amd.h"
 #include "appnp_internal.h"
 
 using appnp::StepArgs;
 
+namespace appnp {
 namespace {
+
+// appnp_kernel_timer_*: one timing event per launch, recorded on the launch's stream
+struct KTimer {
+  bool on = false;
+  int dropped = 0;              // launches past the capacity (not timed)
+  std::vector<hipEvent_t> ev;   // ev[0]: the start event; ev[i]: after launch i
+  std::vector<hipStream_t> st;
+  std::vector<int> kind;
+  int n = 0;                    // events recorded
+
+  void release() {
+    for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+    ev.clear();
+    st.clear();
+    kind.clear();
+    n = dropped = 0;
+    on = false;
+  }
+};
+thread_local KTimer g_ktimer;
+
+}  // namespace
+
+void ktimer_mark(hipStream_t s, int kind) {
+  KTimer& t = g_ktimer;
+  if (!t.on) return;
+  if (t.n >= (int)t.ev.size() || hipEventRecord(t.ev[t.n], s) != hipSuccess) {
+    ++t.dropped;
+    return;
+  }
+  t.st[t.n] = s;
+  t.kind[t.n] = kind;
+  ++t.n;
+}
+
+}  // namespace appnp
+
+namespace {
+
+using appnp::ktimer_mark;
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
@@ -159,6 +202,7 @@ int propagate_split(const appnp_graph* g, const StepArgs& a0, const void* H, int
   float* z = static_cast<float*>(Z);
   int rc = dev_err(appnp::launch_split_copy(h, ld_h, n, f, fs, rw, main_of(0), rem_of(0),
                                             appnp::remainder_scale(g), s));
+  ktimer_mark(s, APPNP_KT_COPY);
   g->rem_launches.fetch_add(K, std::memory_order_relaxed);
   StepArgs am = a0, ar = a0;  // main / remainder chain
   am.f = (int32_t)fs;
@@ -173,7 +217,10 @@ int propagate_split(const appnp_graph* g, const StepArgs& a0, const void* H, int
     am.zin = main_of(cur);
     am.out = last ? Z : main_of(dst);
     am.ld_out = last ? ld_z : fs;
-    if (fs > 0) rc = dev_err(appnp::launch_step(APPNP_F32, appnp::EPI_FWD, 4, am, s));
+    if (fs > 0) {
+      rc = dev_err(appnp::launch_step(APPNP_F32, appnp::EPI_FWD, 4, am, s));
+      ktimer_mark(s, APPNP_KT_STEP);
+    }
     if (rc) break;
     set_drop(ar, p_drop, seed, k);
     // LPE = 1: nv = 4 into the next remainder buffer (the shipped form); LPE > 1: nv is always
@@ -182,6 +229,7 @@ int propagate_split(const appnp_graph* g, const StepArgs& a0, const void* H, int
     rc = dev_err(appnp::launch_remainder(g, ar, appnp::EPI_FWD, rem_of(cur), h + fs, ld_h,
                                          last ? z + fs : rem_of(dst), last ? ld_z : rw, nv,
                                          !last, s));
+    ktimer_mark(s, APPNP_KT_REM);
     cur = dst;
   }
   return rc;
@@ -202,6 +250,7 @@ int propagate_bwd_split(const appnp_graph* g, const StepArgs& a0, const void* dZ
   int rc = dev_err(appnp::launch_split_copy(static_cast<const float*>(dZ), ld_dz, n, f, fs, rw,
                                             main_of(0), rem_of(0), appnp::remainder_scale(g),
                                             s));
+  ktimer_mark(s, APPNP_KT_COPY);
   g->rem_launches.fetch_add(K, std::memory_order_relaxed);
   StepArgs am = a0, ar = a0;  // main / remainder chain
   am.f = (int32_t)fs;
@@ -218,13 +267,17 @@ int propagate_bwd_split(const appnp_graph* g, const StepArgs& a0, const void* dZ
     am.alpha = a_k;
     am.zin = main_of(cur);
     am.out = k == 0 ? nullptr : main_of(dst);
-    if (fs > 0) rc = dev_err(appnp::launch_step(APPNP_F32, appnp::EPI_BWD, 4, am, s));
+    if (fs > 0) {
+      rc = dev_err(appnp::launch_step(APPNP_F32, appnp::EPI_BWD, 4, am, s));
+      ktimer_mark(s, APPNP_KT_STEP);
+    }
     if (rc) break;
     set_drop(ar, p_drop, seed, k);
     ar.alpha = a_k;
     rc = dev_err(appnp::launch_remainder(g, ar, appnp::EPI_BWD, rem_of(cur), dh_rem, ld_dh,
                                          k == 0 ? nullptr : rem_of(dst), rw, (int)(f - fs),
                                          true, s));
+    ktimer_mark(s, APPNP_KT_REM);
     cur = dst;
   }
   return rc;
@@ -420,9 +473,12 @@ int appnp_propagate(const appnp_graph* g, const void* H, int64_t ld_h, void* Z, 
   if (!H || !Z || ld_h < f || ld_z < f || H == Z) return APPNP_EINVAL;
   const hipStream_t s = as_stream(stream);
   const int64_t es = elem_size(dtype);
-  if (K == 0)
-    return dev_err(hipMemcpy2DAsync(Z, ld_z * es, H, ld_h * es, f * es, n,
-                                    hipMemcpyDeviceToDevice, s));
+  if (K == 0) {
+    rc = dev_err(hipMemcpy2DAsync(Z, ld_z * es, H, ld_h * es, f * es, n,
+                                  hipMemcpyDeviceToDevice, s));
+    ktimer_mark(s, APPNP_KT_COPY);
+    return rc;
+  }
   const int64_t ld_w = line_ld(f, dtype);
   void* const ws_orig = ws;
   if (K >= 2) {
@@ -467,6 +523,7 @@ int appnp_propagate(const appnp_graph* g, const void* H, int64_t ld_h, void* Z, 
     a.ld_out = ld_dst;
     set_drop(a, p_drop, seed, k);
     rc = dev_err(appnp::launch_step(dtype, appnp::EPI_FWD, V, a, s));
+    ktimer_mark(s, APPNP_KT_STEP);
     if (rc) return rc;
     src = dst;
     ld_src = ld_dst;
@@ -489,9 +546,12 @@ int appnp_propagate_bwd(const appnp_graph* g, const void* dZ, int64_t ld_dz, voi
   if (!dZ || !dH || ld_dz < f || ld_dh < f || dZ == dH) return APPNP_EINVAL;
   const hipStream_t s = as_stream(stream);
   const int64_t es = elem_size(dtype);
-  if (K == 0)
-    return dev_err(hipMemcpy2DAsync(dH, ld_dh * es, dZ, ld_dz * es, f * es, n,
-                                    hipMemcpyDeviceToDevice, s));
+  if (K == 0) {
+    rc = dev_err(hipMemcpy2DAsync(dH, ld_dh * es, dZ, ld_dz * es, f * es, n,
+                                  hipMemcpyDeviceToDevice, s));
+    ktimer_mark(s, APPNP_KT_COPY);
+    return rc;
+  }
   const int64_t ld_w = line_ld(f, dtype);
   const int64_t buf = n * ld_w * es;
   const int nbuf = K >= 3 ? 2 : (K == 2 ? 1 : 0);
@@ -512,6 +572,7 @@ int appnp_propagate_bwd(const appnp_graph* g, const void* dZ, int64_t ld_dz, voi
   // dH = alpha * dZ  (the k = K term), then G_k = (1-alpha) M_k^T G_{k+1},
   // dH += alpha G_k (k >= 1) / dH += G_0.
   rc = dev_err(appnp::launch_scale_rows(dtype, dZ, ld_dz, dH, ld_dh, n, f, alpha, s));
+  ktimer_mark(s, APPNP_KT_COPY);
   if (rc) return rc;
   // split rows (self-adjoint A_hat: the source-blocked copy of A_hat is that of A_hat^T)
   const int64_t dd_lds[2] = {ld_dz, ld_dh};
@@ -555,6 +616,7 @@ int appnp_propagate_bwd(const appnp_graph* g, const void* dZ, int64_t ld_dz, voi
     a.alpha = k >= 1 ? alpha : 1.0f;
     set_drop(a, p_drop, seed, k);
     rc = dev_err(appnp::launch_step(dtype, appnp::EPI_BWD, V, a, s));
+    ktimer_mark(s, APPNP_KT_STEP);
     if (rc) return rc;
     src = dst;
     ld_src = ld_w;
@@ -648,7 +710,9 @@ int appnp_step(const appnp_graph* g, int part, const void* Zin, int64_t ld_in, c
     }
   }
   const int V = appnp::pick_vec(dtype, f, lds, n_ld, ptrs, 4);
-  return dev_err(appnp::launch_step(dtype, epi, V, a, as_stream(stream)));
+  rc = dev_err(appnp::launch_step(dtype, epi, V, a, as_stream(stream)));
+  ktimer_mark(as_stream(stream), APPNP_KT_STEP);
+  return rc;
 }
 
 // ---- the split layout on the held rows of a row-partitioned graph -------------------------
@@ -681,10 +745,13 @@ int appnp_split_copy(const appnp_graph* g, const float* H, int64_t ld_h, int64_t
   const void* ptrs[3] = {H, main, rem};
   if (!H || !rem || (fs > 0 && !main) || ld_h < f || !vec16(lds, 1, ptrs, 3)) return APPNP_EINVAL;
   const float* sc = appnp::remainder_scale(g);
-  return dev_err(appnp::launch_split_copy(H, ld_h, rows, f, fs, rw,
-                                          main ? main + g->row_lo * fs : nullptr,
-                                          rem + g->row_lo * rw, sc ? sc + g->row_lo : nullptr,
-                                          as_stream(stream)));
+  const int rc = dev_err(appnp::launch_split_copy(H, ld_h, rows, f, fs, rw,
+                                                  main ? main + g->row_lo * fs : nullptr,
+                                                  rem + g->row_lo * rw,
+                                                  sc ? sc + g->row_lo : nullptr,
+                                                  as_stream(stream)));
+  ktimer_mark(as_stream(stream), APPNP_KT_COPY);
+  return rc;
 }
 
 int appnp_step_split(const appnp_graph* g, int part, const float* zin_main, const float* zin_rem,
@@ -752,6 +819,7 @@ int appnp_step_split(const appnp_graph* g, int part, const float* zin_main, cons
       }
     }
     rc = dev_err(appnp::launch_step(APPNP_F32, epi, 4, am, s));
+    ktimer_mark(s, APPNP_KT_STEP);
     if (rc) return rc;
   }
   if (part == APPNP_PART_LOCAL) return APPNP_OK;  // the pass needs every row of zin_rem
@@ -759,9 +827,57 @@ int appnp_step_split(const appnp_graph* g, int part, const float* zin_main, cons
   // rows (a unit graph stores dr o y there), or into Z's last r columns
   const int nv = (g->rb_lpe == 1 && !to_z) ? 4 : (int)r;
   g->rem_launches.fetch_add(1, std::memory_order_relaxed);
-  return dev_err(appnp::launch_remainder(g, a, appnp::EPI_FWD, zin_rem, H + fs, ld_h,
-                                         to_z ? Z + fs : zout_rem + g->row_lo * rw,
-                                         to_z ? ld_z : rw, nv, !to_z, s));
+  rc = dev_err(appnp::launch_remainder(g, a, appnp::EPI_FWD, zin_rem, H + fs, ld_h,
+                                       to_z ? Z + fs : zout_rem + g->row_lo * rw,
+                                       to_z ? ld_z : rw, nv, !to_z, s));
+  ktimer_mark(s, APPNP_KT_REM);
+  return rc;
+}
+
+// ---- the per-launch timer (measurement aid; include/ppnp_amd.h) ----------------------------
+
+int appnp_kernel_timer_begin(int max_launches, void* stream) {
+  appnp::KTimer& t = appnp::g_ktimer;
+  if (max_launches < 1 || max_launches > (1 << 20)) return APPNP_EINVAL;
+  t.release();
+  t.ev.assign((size_t)max_launches + 1, nullptr);
+  t.st.assign(t.ev.size(), nullptr);
+  t.kind.assign(t.ev.size(), 0);
+  for (hipEvent_t& e : t.ev) {
+    if (hipEventCreate(&e) != hipSuccess) {
+      e = nullptr;
+      t.release();
+      return APPNP_EDEVICE;
+    }
+  }
+  t.on = true;
+  ktimer_mark(as_stream(stream), 0);  // the start event
+  if (t.n != 1) {
+    t.release();
+    return APPNP_EDEVICE;
+  }
+  return APPNP_OK;
+}
+
+int appnp_kernel_timer_end(float* ms, int* kinds, int max, int* n_out) {
+  appnp::KTimer& t = appnp::g_ktimer;
+  if (!t.on) return APPNP_EINVAL;
+  t.on = false;
+  int rc = APPNP_OK;
+  for (int i = 0; i < t.n && rc == APPNP_OK; ++i) rc = dev_err(hipEventSynchronize(t.ev[i]));
+  const int launches = t.n - 1;
+  for (int i = 1; i < t.n && i - 1 < max && rc == APPNP_OK; ++i) {
+    int j = i - 1;  // the previous event on the same stream
+    while (j >= 0 && t.st[j] != t.st[i]) --j;
+    float e = NAN;
+    if (j >= 0 && hipEventElapsedTime(&e, t.ev[j], t.ev[i]) != hipSuccess) e = NAN;
+    if (ms) ms[i - 1] = e;
+    if (kinds) kinds[i - 1] = t.kind[i];
+  }
+  if (n_out) *n_out = launches;
+  if (rc == APPNP_OK && t.dropped) rc = APPNP_ERANGE;
+  t.release();
+  return rc;
 }
 
 // ---- captured plans: the K launches of appnp_propagate replayed as one hipGraph -----------

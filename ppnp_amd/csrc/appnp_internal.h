@@ -113,6 +113,11 @@ hipError_t launch_step(int dtype, int epi, int V, const StepArgs& a, hipStream_t
 hipError_t launch_scale_rows(int dtype, const void* src, int64_t ld_src, void* dst,
                              int64_t ld_dst, int64_t n, int64_t f, float alpha, hipStream_t s);
 
+// appnp_capi.hip: the per-launch timer of appnp_kernel_timer_begin / _end.  While it is on
+// (on this thread), every launch of the propagation entry points is followed by a timing event
+// on its stream, tagged with the launch's kind (APPNP_KT_*).  Off: one thread-local load.
+void ktimer_mark(hipStream_t s, int kind);
+
 // Leading dimension of the internal ping-pong buffers.  A random row gather costs 128-B line
 // requests, not bytes, so rows are padded to start on a line
 // (next power of two up to one line, then whole lines) -- but only when that lowers the

@@ -226,6 +226,30 @@ class PropagatePlan:
             pass
 
 
+KERNEL_KINDS = {_lib.KT_COPY: "copy", _lib.KT_STEP: "step", _lib.KT_REM: "rem"}
+
+
+def kernel_times(fn, device, max_launches: int = 1024) -> list[tuple[str, float]]:
+    """Call ``fn()`` with the library's per-launch timer on (``appnp_kernel_timer_begin`` /
+    ``_end``) and return one (kind, ms) pair per launch it enqueued, in launch order: "copy"
+    (the split copy), "step" (the SpMM kernel), "rem" (the remainder pass).  The events sit on
+    the launch stream between launches that are stream-ordered anyway; no profiler runs."""
+    lib = _lib.load()
+    with torch.cuda.device(device):
+        _lib.check("appnp_kernel_timer_begin",
+                   lib.appnp_kernel_timer_begin(int(max_launches), _stream(device)))
+        try:
+            fn()
+        finally:
+            ms = (C.c_float * max_launches)()
+            kinds = (C.c_int * max_launches)()
+            n = C.c_int(0)
+            rc = lib.appnp_kernel_timer_end(ms, kinds, max_launches, C.byref(n))
+        _lib.check("appnp_kernel_timer_end", rc)
+    return [(KERNEL_KINDS.get(kinds[i], str(kinds[i])), float(ms[i]))
+            for i in range(min(n.value, max_launches))]
+
+
 def line_rate_probe(table: torch.Tensor, lines: int, seed: int = 0, reps: int = 3) -> dict:
     """The device's random 128-B line rate (``appnp_line_rate_probe``): ``lines`` random lines
     gathered from ``table``'s storage (read only) per launch, one warm-up launch, then the

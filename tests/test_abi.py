@@ -76,6 +76,19 @@ def test_line_rate_probe_validates_arguments():
                                      None) == _lib.APPNP_OK  # nothing to do
 
 
+def test_kernel_timer_validates_arguments():
+    """appnp_kernel_timer_begin / _end: bad capacities and an end without a begin return codes
+    before any device call."""
+    from ppnp_amd import _lib
+
+    lib = _lib.load()
+    n = C.c_int(-1)
+    assert lib.appnp_kernel_timer_begin(0, None) == _lib.APPNP_EINVAL
+    assert lib.appnp_kernel_timer_begin(-3, None) == _lib.APPNP_EINVAL
+    assert lib.appnp_kernel_timer_begin(1 << 21, None) == _lib.APPNP_EINVAL
+    assert lib.appnp_kernel_timer_end(None, None, 0, C.byref(n)) == _lib.APPNP_EINVAL
+
+
 def test_argument_validation_without_device():
     """Errors are returned as codes, never raised/aborted across the ABI."""
     from ppnp_amd import _lib

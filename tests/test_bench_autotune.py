@@ -32,11 +32,14 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, plan, out, timeout_s):
+def _worker(rank, world, port, plan, out, timeout_s, budget_s=0.0):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import bench
+
+    bench.MIN_CANDIDATE_S = 0.5  # the budget's floor, scaled to the stubs' seconds
+    t_start = time.monotonic() - 0.1 * rank  # the ranks' clocks differ: they agree on the max
 
     def measure(tag):
         delay, who, what = plan[tag]
@@ -64,7 +67,9 @@ def _worker(rank, world, port, plan, out, timeout_s):
 
     try:
         best, times = bench.run_candidates(list(plan), measure, None, timeout_s, emit,
-                                           lambda t: t, rank, world, abort=lambda: None)
+                                           lambda t: t, rank, world, abort=lambda: None,
+                                           budget_s=budget_s,
+                                           age=lambda: time.monotonic() - t_start)
         if rank == 0:
             emit(best)
     except RuntimeError as e:
@@ -73,10 +78,10 @@ def _worker(rank, world, port, plan, out, timeout_s):
         dist.destroy_process_group()
 
 
-def _run(plan, tmp_path, world=2, timeout_s=60.0):
+def _run(plan, tmp_path, world=2, timeout_s=60.0, budget_s=0.0):
     out = str(tmp_path / "line")
-    mp.start_processes(_worker, args=(world, _free_port(), plan, out, timeout_s), nprocs=world,
-                       join=True, start_method="spawn")
+    mp.start_processes(_worker, args=(world, _free_port(), plan, out, timeout_s, budget_s),
+                       nprocs=world, join=True, start_method="spawn")
     res = {}
     for r in range(world):
         if os.path.exists(f"{out}.{r}"):
@@ -138,6 +143,40 @@ def test_peer_gone_during_agreement_still_prints_the_line(tmp_path):
     line = res[0]
     assert line["tag"] == "col"
     assert line["config"]["autotune_ms_per_step"]["2x4-multipath"] == "timeout"
+
+
+def test_run_budget_skips_candidates_and_prints_the_column_line(tmp_path):
+    """slow-but-not-stalled candidates cannot together outlast the driver's
+    timeout.  With a 3 s budget the first exchange candidate (2.7 s) is measured, then less than
+    MIN_CANDIDATE_S is left: the rest are skipped on both ranks, rank 0 prints the fastest line
+    (the column layout's) and both processes exit 0."""
+    plan = {"col": (0.02, None, None), "row": (2.7, None, None), "2x1": (0.01, None, None),
+            "1x2": (0.01, None, None)}
+    t0 = time.time()
+    res = _run(plan, tmp_path, timeout_s=60.0, budget_s=3.0)
+    assert time.time() - t0 < 60
+    assert list(res) == [0]
+    line = res[0]
+    assert line["tag"] == "col"
+    times = line["config"]["autotune_ms_per_step"]
+    assert times["row"] >= 2700.0
+    assert times["2x1"] == times["1x2"] == "skipped: run budget"
+
+
+def test_run_budget_cuts_a_running_candidate_short(tmp_path):
+    """A candidate that starts with budget left but would run past it is ended by a deadline of
+    the budget left (not the much longer candidate timeout): the column line is printed, the
+    candidate marked "timeout", and both processes exit 0."""
+    plan = {"col": (0.02, None, None), "row": (1.0, None, None), "2x1": (30.0, None, None),
+            "never": (0.0, None, None)}
+    t0 = time.time()
+    res = _run(plan, tmp_path, timeout_s=120.0, budget_s=3.0)
+    assert time.time() - t0 < 60
+    assert list(res) == [0]
+    line = res[0]
+    assert line["tag"] == "col"
+    times = line["config"]["autotune_ms_per_step"]
+    assert times["2x1"] == "timeout" and "never" not in times
 
 
 if __name__ == "__main__":
