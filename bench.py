@@ -24,7 +24,7 @@ Extra JSON fields:
                 section 8(d), restricted to the rank's share) / the average iteration time,
                 measured with HIP events on the launch stream; peak 8 TB/s.  ``ceiling`` is
                 the access-pattern floor of the iteration time (line requests beyond L2 at the
-                fastest measured random-line rate, the remainder pass at its measured rate;
+                fastest measured random-line rate, the remainder pass's count floor;
                 exchange at the xGMI link peak).  ``traffic``: committed PMC bytes of the
                 rank's kernels.  ``box_line_rate``: this GPU's random-line rate, probed right
                 before the timed region.
@@ -58,23 +58,29 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip-level param
 GATHER_LINE_CEILING = 60.0
 # xGMI: 7 links per GPU at 76.8 GB/s per direction (153.6 GB/s bidirectional)
 XGMI_IN_GBS = 7 * 76.8
-# The persistent remainder pass (appnp_blocks.hip), MEASURED: the fastest G nonzeros/s of one
-# W-column pass over products-synth's shape (126-127 M nonzeros, 2.45 M rows), its row passes
-# and entry stream included.  W4: the probe, tools/blk_probe.hip 0.680 ms for 127.3 M
-# (profiles/r2_blk_probe.txt; the library's pass takes 0.766 ms).  W8 / W16: the library's own
-# pass since round 4's barrier every 32 blocks, faster than the round-2 probe (1.165 / 1.894 ms):
-# F = 40's W8 pass 1.105 ms and the 8-rank column slab's W16 pass 1.769 ms for 126.2 M
-# (profiles/r4_sync_ab.txt).  The arxiv shape (one row pass) is no faster.  Its gathers are L2
-# requests and its cost is set by the L2 misses of the block sweep and the row passes
-# (DESIGN.md 4.2, 9), so no byte peak prices it (the 34.5 TB/s L2 byte peak
-# put the 13-column slab's floor at 0.35 ms).
-REM_PASS_RATE = {4: 187.4, 8: 114.2, 16: 71.3}
-REM_PASS_SOURCE = "profiles/r2_blk_probe.txt (W4), profiles/r4_sync_ab.txt (W8, W16)"
+# The persistent remainder pass (appnp_blocks.hip): its floor from COUNTS, independent of the
+# pass's own timings (round 4 priced it at its own fastest time, so the
+# 8-rank column slab's ceiling certified the kernel against itself).  Two terms, the larger wins:
+#   * fill: every XCD's L2 must take in the whole remainder table once per row pass --
+#     row passes x 8 XCDs x n x 16 LPE bytes / 128-B lines, at the fastest measured random-line
+#     rate (GATHER_LINE_CEILING) -- plus the entry stream (4 B per entry: value-free) at the HBM
+#     peak, both from beyond L2;
+#   * requests: one L2 request per nonzero (an entry's 16 LPE bytes lie in one line) at the rate
+#     of the W4 pass with every gather forced to an L2-resident row: 0.665 ms for products-synth's
+#     126,165,965 nonzeros, entry stream included = 189.7 G requests/s.
+# Row passes: ceil(rows / (CUs x 16 waves x 640 / LPE rows)), as graph_build_source_blocks has it.
+REM_L2_REQ_RATE = 126_165_965 / 0.665e-3 / 1e9
+REM_L2_REQ_SOURCE = ("DESIGN.md 4.2: the W4 pass with every gather an L2 hit, 0.665 ms for "
+                     "126.2 M nonzeros")
+XCDS, CUS, REM_WAVES, REM_ROWS_LPE1 = 8, 256, 16, 640
 # N > 1: the whole run's wall budget, below the driver's 600 s bench timeout with
 # room for the launcher, the first `import torch` of a fresh box and the teardown; a candidate
 # is not started with less than MIN_CANDIDATE_S of it left
 RUN_BUDGET_S = 420.0
 MIN_CANDIDATE_S = 20.0
+# N > 1: the largest oracle Z_K (fp32 bytes) rank 0 sends to every rank for the parity check
+# (products-synth: 0.98 GB, ~2-4 s over gloo on one host)
+PARITY_BCAST_MAX_BYTES = 4 << 30
 # The in-library line-rate probe run before the timed region (appnp_line_rate_probe): random
 # 128-B lines gathered from the bench's own H buffer, ~20 ms
 PROBE_LINES = 1 << 30
@@ -286,6 +292,22 @@ def rank_traffic_key(workload, dtype_name, runner, K) -> str:
                        bool(getattr(runner, "overlap", False)))
 
 
+def remainder_floor(n, rows, nnz, lpe):
+    """The W = 4 lpe remainder pass's floor from counts (see REM_L2_REQ_RATE): the larger of its
+    compulsory L2 fill (+ entry stream) from beyond L2 and its L2 requests at the all-hit rate."""
+    slot_rows = CUS * REM_WAVES * (REM_ROWS_LPE1 // lpe)
+    passes = max(1, -(-rows // slot_rows))
+    fill_lines = passes * XCDS * n * 16 * lpe / 128
+    entry_bytes = 4 * nnz
+    fill_ms = (fill_lines / (GATHER_LINE_CEILING * 1e9) + entry_bytes / (HBM_PEAK_GBS * 1e9)) * 1e3
+    req_ms = nnz / (REM_L2_REQ_RATE * 1e9) * 1e3
+    return {"ms": max(fill_ms, req_ms), "fill_ms": fill_ms, "l2_request_ms": req_ms,
+            "row_passes": passes, "fill_lines": fill_lines,
+            "kind": "count floor (not a measured rate): max(row passes x 8 XCDs x table / 128-B "
+                    f"lines at {GATHER_LINE_CEILING} G lines/s + 4 B/entry at the HBM peak, "
+                    f"one L2 request per nonzero at {REM_L2_REQ_RATE:.1f} G/s ({REM_L2_REQ_SOURCE}))"}
+
+
 def roofline(*, n, rows, nnz, F_local, esz, avg_iter_ms, fs, r, lpe, exchange_in_bytes=0,
              kernel="", kernel_key="", traffic=None):
     """The roofline block of one rank.
@@ -298,8 +320,8 @@ def roofline(*, n, rows, nnz, F_local, esz, avg_iter_ms, fs, r, lpe, exchange_in
       * the SpMM kernel's line requests beyond L2 at the fastest measured random-line rate --
         ``lines_per_nonzero`` gathered 128-B lines per nonzero (whole lines of the fs main
         columns, or all of a whole row) plus its streamed bytes (CSR, H, Z) / 128 -- plus, with
-        split rows, the remainder pass's nonzeros at that pass's MEASURED rate for its width
-        (``REM_PASS_RATE``: the probe of the same pass, row passes and entry stream included);
+        split rows, the remainder pass's floor from counts (``remainder_floor``: its L2 fill per
+        row pass and its L2 requests, not its own measured time);
       * a row layout's exchange: the bytes landing here / the xGMI links' peak;
       * B_iter at the HBM peak (the roofline itself), so ceiling.frac <= 1.
     So frac <= ceiling.frac <= 1 on a uniform random graph, up to the probe's own spread; a
@@ -321,8 +343,8 @@ def roofline(*, n, rows, nnz, F_local, esz, avg_iter_ms, fs, r, lpe, exchange_in
         dense = 2 * rows * ld * s
     lines = nnz * lpn + (stream + dense) / 128
     width = 4 * lpe
-    rem_rate = REM_PASS_RATE[width] if r else None
-    rem_ms = nnz / (rem_rate * 1e9) * 1e3 if r else 0.0
+    rem = remainder_floor(n, rows, nnz, lpe) if r else None
+    rem_ms = rem["ms"] if r else 0.0
     compute_ms = lines / (GATHER_LINE_CEILING * 1e9) * 1e3 + rem_ms
     exchange_ms = exchange_in_bytes / (XGMI_IN_GBS * 1e9) * 1e3
     hbm_ms = b_iter / (HBM_PEAK_GBS * 1e9) * 1e3
@@ -367,15 +389,16 @@ def roofline(*, n, rows, nnz, F_local, esz, avg_iter_ms, fs, r, lpe, exchange_in
             "remainder_l2_requests_per_nonzero": lpe if r else 0,
             "compute_ms": compute_ms,
             "remainder_pass_ms": rem_ms,
-            "remainder_pass_rate_G_nnz_s": rem_rate,
+            "remainder_pass_floor": rem,
             "exchange_ms": exchange_ms,
             "hbm_ms": hbm_ms,
             "exchange_in_bytes": exchange_in_bytes,
             "clamped_to_measured": clamped,
             "basis": f"max of: {lines:.4g} line requests per iteration at "
                      f"{GATHER_LINE_CEILING} G lines/s"
-                     + (f" + {nnz:.4g} nonzeros through the W{width} remainder pass at its "
-                        f"measured {rem_rate} G nonzeros/s ({REM_PASS_SOURCE})" if r else "")
+                     + (f" + the W{width} remainder pass's count floor for {nnz:.4g} "
+                        f"nonzeros ({rem['row_passes']} row passes; remainder_pass_floor)"
+                        if r else "")
                      + f"; exchange {exchange_in_bytes / 1e6:.4g} MB in at "
                        f"{XGMI_IN_GBS:.0f} GB/s; B_iter at the HBM peak",
         },
@@ -844,7 +867,11 @@ def main(argv=None):
         Gref.close()
         del Gref
         torch.cuda.empty_cache()
-    use_oracle = cpu_iters == K and not args.emulate
+    # the oracle's Z_K goes to every rank's host memory: above PARITY_BCAST_MAX_BYTES (ADVICE
+    # r4: it grows with n x F and only the gloo timeout bounds the broadcast) the lines fall back
+    # to the single-GPU reference, and the CPU leg still gives cpu_baseline
+    use_oracle = (cpu_iters == K and not args.emulate
+                  and (world == 1 or n * F * 4 <= PARITY_BCAST_MAX_BYTES))
     if world > 1 and use_oracle:
         have = torch.tensor([1 if Zc is not None else 0], dtype=torch.int32)
         torch.distributed.broadcast(have, 0, group=ctl)

@@ -88,10 +88,10 @@ enum appnp_norm { APPNP_NORM_SYM = 0, APPNP_NORM_RW = 1 };
 enum appnp_dtype { APPNP_F32 = 0, APPNP_BF16 = 1 };
 
 int appnp_abi_version(void);
-/* Provenance of this build: "src=<digest of the .hip and .h files of ppnp_amd/csrc
- * (srcdigest.py)>;abi=..;
- * arch=gfx950;compiler=..;built=..".  bench.py prints it next to the digest of the tree it
- * runs in, so a library built from other sources shows. */
+/* Provenance of this build: "src=<digest of the .hip and .h files of ppnp_amd/csrc and of this
+ * header (srcdigest.py)>;abi=..;arch=<the Makefile's ARCH, gfx950>;compiler=..;built=..".
+ * bench.py prints it next to the digest of the tree it runs in, so a library built from other
+ * sources shows. */
 const char* appnp_build_info(void);
 const char* appnp_strerror(int code);
 
@@ -332,10 +332,13 @@ typedef int (*appnp_allgather_fn)(void* buf, size_t shard_bytes, int rank, int n
  * none: the rule is the same on every rank (its gather-locality measure is taken over the whole
  * A), and since the copy is best-effort, the first fp32 propagation with K >= 2 agrees through
  * one small exchange in the workspace that every rank built it (that call synchronises the
- * stream once), and a rank whose agreement fails keeps failing (the handle is poisoned: every
- * later call returns the error).  ld_h and ld_z must be the same on every rank: with both a
- * multiple of 4 the split layout runs, and a rank whose H or Z is then not 16-B aligned gets
- * APPNP_EINVAL (its peers would split); otherwise every rank gathers whole rows.
+ * stream once).  A rank whose agreement fails after that exchange keeps failing (the handle is
+ * poisoned: every later call returns the stored error without exchanging); a failure before it
+ * (the flag's memset, or the callback itself) leaves the peers waiting in that exchange, as
+ * any collective does when one rank drops out, so the caller must then end its communicator.
+ * The decision does not depend on H or Z: a rank whose H or Z is not 16-B aligned (base pointer
+ * or leading dimension) stages it through the workspace, so every rank exchanges the same
+ * parts.
  * overlap != 0 keeps the held rows as local- and remote-column CSRs (fp32 propagation only).
  * allgather/ctx: the exchange, called by every rank once per exchanged iterate (twice on the
  * split layout: its main part, then its remainder part). */
@@ -349,7 +352,8 @@ const appnp_graph* appnp_dist_graph(const appnp_dist* d);
 
 /* Workspace of appnp_dist_propagate: two full-height iterates (P S rows, line-aligned, or the
  * two parts of the split layout) and, with overlap, the fp32 local-column partial of the held
- * rows; the larger of the two layouts when F splits. */
+ * rows; the larger of the two layouts when F splits, the split one with room to stage a
+ * misaligned H and Z ([S, F rounded up to 4] fp32 each). */
 size_t appnp_dist_workspace_bytes(const appnp_dist* d, int64_t f, int dtype);
 
 /*

@@ -295,9 +295,13 @@ int appnp_abi_version(void) { return PPNP_AMD_ABI_VERSION; }
 #define APPNP_STR2(x) #x
 #define APPNP_STR(x) APPNP_STR2(x)
 
+#ifndef APPNP_ARCH
+#define APPNP_ARCH "unknown"
+#endif
+
 const char* appnp_build_info(void) {
-  return "src=" APPNP_SRC_DIGEST ";abi=" APPNP_STR(PPNP_AMD_ABI_VERSION) ";arch=gfx950;compiler="
-      __VERSION__ ";built=" __DATE__ " " __TIME__;
+  return "src=" APPNP_SRC_DIGEST ";abi=" APPNP_STR(PPNP_AMD_ABI_VERSION) ";arch=" APPNP_ARCH
+      ";compiler=" __VERSION__ ";built=" __DATE__ " " __TIME__;
 }
 
 const char* appnp_strerror(int code) {

@@ -73,6 +73,10 @@ struct WsLayout {
   // split rows: main [P S, fs] and remainder [P S, rw] parts of each iterate
   int64_t fs = 0, rw = 0;
   size_t main_bytes = 0, part_bytes = 0;  // one main part; one iterate (main + remainder)
+  // staging of a held-rows H or Z whose base or leading dimension does not allow 16-B vectors:
+  // [S, f4] fp32 each (f4 = f rounded up to 4), after the iterates and the partial
+  int64_t f4 = 0;
+  size_t stage_off = 0, stage_bytes = 0;
   size_t split_total = 0;
 };
 
@@ -88,7 +92,10 @@ WsLayout ws_layout(const appnp_dist* d, int64_t f, int dtype) {
   if (dtype == APPNP_F32 && appnp_split_layout(d->g, f, &w.fs, &w.rw) == APPNP_OK) {
     w.main_bytes = align_up(rows_pad * (size_t)w.fs * 4);
     w.part_bytes = w.main_bytes + align_up(rows_pad * (size_t)w.rw * 4);
-    w.split_total = 2 * w.part_bytes + (d->overlap ? align_up((size_t)d->shard * w.fs * 4) : 0);
+    w.f4 = (f + 3) / 4 * 4;
+    w.stage_off = 2 * w.part_bytes + (d->overlap ? align_up((size_t)d->shard * w.fs * 4) : 0);
+    w.stage_bytes = align_up((size_t)d->shard * (size_t)w.f4 * 4);
+    w.split_total = w.stage_off + 2 * w.stage_bytes;
   }
   return w;
 }
@@ -115,6 +122,10 @@ int agree_split(appnp_dist* d, void* ws, hipStream_t s) {
   if (rc == APPNP_OK && d->split_ok)
     rc = dev_err(hipMemsetAsync(flags + kSlot * d->rank, 1, 1, s));
   if (rc == APPNP_OK) rc = d->allgather(flags, kSlot, d->rank, d->nranks, s, d->ctx);
+  // APPNP_DIST_TEST_AGREE_FAIL (tests): a failure on this rank after the exchange, so the
+  // poisoned handle can be observed
+  const char* inj = std::getenv("APPNP_DIST_TEST_AGREE_FAIL");
+  if (rc == APPNP_OK && inj && *inj && std::atoi(inj)) rc = APPNP_EDEVICE;
   for (int p = 0; p < d->nranks && rc == APPNP_OK; ++p)
     rc = dev_err(hipMemcpyAsync(&host[p], flags + kSlot * p, 1, hipMemcpyDeviceToHost, s));
   if (rc == APPNP_OK) rc = dev_err(hipStreamSynchronize(s));
@@ -292,16 +303,36 @@ int appnp_dist_propagate(appnp_dist* d, const void* H, int64_t ld_h, void* Z, in
     const int arc = agree_split(d, ws, s);
     if (arc != APPNP_OK) return arc;
   }
-  // split rows when every rank's copy allows it and the leading dimensions allow 16-B vectors
-  // (K >= 2: one iteration gains nothing from the split layout).  Collective: ld_h / ld_z are
-  // the same on every rank (include/ppnp_amd.h), so that part of the decision agrees; a base
-  // pointer that is not 16-B aligned is this rank's alone, and the rank reports it instead of
-  // silently exchanging one part per iterate where its peers exchange two
-  if (d->split_ok && w.split_total && K >= 2 && ld_h % 4 == 0 && ld_z % 4 == 0) {
-    if (rows > 0 && !(aligned16(H, ld_h) && aligned16(Z, ld_z))) return APPNP_EINVAL;
+  // split rows whenever every rank's copy allows it (K >= 2: one iteration gains nothing from
+  // the split layout).  The decision depends only on what the ranks agreed on, so every rank
+  // exchanges the same parts: an H or Z whose base pointer or leading dimension does not allow
+  // 16-B vectors is this rank's alone, and it is staged through the workspace ([S, f4] fp32,
+  // copied in before the loop and out after it) rather than changing this rank's path (ADVICE
+  // r4: round 4 returned APPNP_EINVAL there while the peers waited in the split loop's exchange)
+  if (d->split_ok && w.split_total && K >= 2) {
     if (!ws || ws_bytes < w.split_total) return APPNP_EINVAL;
-    return propagate_split_rows(d, w, static_cast<const float*>(H), ld_h, static_cast<float*>(Z),
-                                ld_z, f, K, alpha, p_drop, seed, static_cast<char*>(ws), s);
+    char* base = static_cast<char*>(ws);
+    const float* h = static_cast<const float*>(H);
+    float* z = static_cast<float*>(Z);
+    int64_t lh = ld_h, lz = ld_z;
+    const bool stage_h = rows > 0 && !aligned16(H, ld_h);
+    const bool stage_z = rows > 0 && !aligned16(Z, ld_z);
+    float* hs = reinterpret_cast<float*>(base + w.stage_off);
+    float* zs = reinterpret_cast<float*>(base + w.stage_off + w.stage_bytes);
+    int rc = APPNP_OK;
+    if (stage_h) {
+      rc = dev_err(copy_rows(hs, w.f4, H, ld_h, rows, f, 4, s));
+      h = hs;
+      lh = w.f4;
+    }
+    if (stage_z) {
+      z = zs;
+      lz = w.f4;
+    }
+    if (rc == APPNP_OK)
+      rc = propagate_split_rows(d, w, h, lh, z, lz, f, K, alpha, p_drop, seed, base, s);
+    if (rc == APPNP_OK && stage_z) rc = dev_err(copy_rows(Z, ld_z, zs, w.f4, rows, f, 4, s));
+    return rc;
   }
   if (!ws || ws_bytes < w.total) return APPNP_EINVAL;
   char* base = static_cast<char*>(ws);
