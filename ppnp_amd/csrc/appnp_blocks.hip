@@ -102,7 +102,18 @@ struct RemLayout {
   int32_t nb, br_log2, slots, rg, passes;
   int32_t scale_out;    // VF: the output is the next remainder buffer (store dr o y)
   int32_t sync;         // > 0: workgroup barrier after every `sync` source blocks (k_rem_persist)
+  int32_t pace;         // > 0 (with sync): XCD-wide pacing at those barriers, slack pace - 1
+                        // barrier periods (rem_pace; measurement override, off by default)
 };
+
+// XCD-wide pacing of k_rem_persist (L.pace > 0): per-XCD arrival and member counters, each on a
+// 128-B line of its own, and a done counter by which the last workgroup of a launch resets them.
+// Pacing only ever delays a workgroup, by a bounded wait, so a stale or disturbed counter (a
+// concurrent launch on another stream, a workgroup not resident) costs time, never results.
+constexpr int kPaceStride = 32;  // uint32 per 128-B line
+constexpr int kPaceXcds = 8;
+__device__ uint32_t g_rem_pace[(2 * kPaceXcds + 1) * kPaceStride];
+constexpr int kPaceSpinMax = 4096;  // polls (s_sleep 2 each: ~4 us) before a wait gives up
 
 // ---- segmented inclusive scan over the 64 lanes (rows non-decreasing across lanes) --------
 // DPP (gfx9 family): row_shr:n shifts within each 16-lane row; row_bcast:15 / row_bcast:31
@@ -280,6 +291,9 @@ __device__ __forceinline__ void rem_walk(const StepArgs& a, const RemLayout& L,
         const int64_t e = (int64_t)(c + u) * CH + le;
         cb[u] = L.cblk[c + u] << L.br_log2;
         en[u] = ld_nt<uint32_t>(L.ent + e);
+#ifdef APPNP_REM_TEST_ALLHIT
+        cb[u] = 0;  // measurement only (tools/build_variant.sh): every gather hits block 0
+#endif
         if constexpr (!VF) wt[u] = ld_nt<float>(L.val + e);
       }
     }
@@ -348,6 +362,16 @@ __global__ __launch_bounds__(kRemThreads) void k_rem_persist(StepArgs a, RemLayo
   f32x4* acc = rem_acc + (int64_t)wv * L.rg * LPE;
   const f32x4* __restrict__ z = static_cast<const f32x4*>(a.zin);
   const int64_t slot = (int64_t)blockIdx.x * kRemWaves + wv;
+  // XCD-wide pacing: this workgroup's XCD and its counters (thread 0 only)
+  uint32_t* arrive = nullptr;
+  uint32_t* members = nullptr;
+  uint32_t epoch = 0;
+  if (L.pace > 0 && threadIdx.x == 0) {
+    const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20) & (kPaceXcds - 1);  // XCC_ID
+    arrive = g_rem_pace + xcc * kPaceStride;
+    members = g_rem_pace + (kPaceXcds + xcc) * kPaceStride;
+    __hip_atomic_fetch_add(members, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   for (int p = 0; p < L.passes; ++p) {
     const int64_t g = (int64_t)p * L.slots + slot;
     const int64_t r0 = g * L.rg;
@@ -359,6 +383,26 @@ __global__ __launch_bounds__(kRemThreads) void k_rem_persist(StepArgs a, RemLayo
       for (int b = 0; b < L.nb; b += L.sync) {
         rem_walk<U, VF, LPE>(a, L, z, acc, r0, L.off[g * L.nb + b] / CH,
                              L.off[g * L.nb + min(b + L.sync, L.nb)] / CH);
+        if (L.pace > 0) {
+          __syncthreads();  // this workgroup's waves are done with the period
+          if (threadIdx.x == 0) {
+            // arrive, then wait (bounded) until the XCD's workgroups have, on average, finished
+            // all but pace - 1 of the periods this one has
+            ++epoch;
+            __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t lag = (uint32_t)(L.pace - 1);
+            if (epoch > lag) {
+              const uint32_t m = __hip_atomic_load(members, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+              const uint32_t need = (epoch - lag) * m;
+              for (int spin = 0; spin < kPaceSpinMax; ++spin) {
+                if (__hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need)
+                  break;
+                __builtin_amdgcn_s_sleep(2);
+              }
+            }
+          }
+        }
         __syncthreads();
       }
     } else {
@@ -370,6 +414,17 @@ __global__ __launch_bounds__(kRemThreads) void k_rem_persist(StepArgs a, RemLayo
     } else {
       for (int r = lane; r < rows * LPE; r += kWave)
         rem_finish_piece<EPI, VF, LPE>(a, L, r0 + r / LPE, r % LPE, acc[r]);
+    }
+  }
+  if (L.pace > 0 && threadIdx.x == 0) {
+    // the launch's last workgroup (every other one is past its last wait) resets the counters
+    uint32_t* done = g_rem_pace + 2 * kPaceXcds * kPaceStride;
+    if (__hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+        gridDim.x - 1) {
+      for (int x = 0; x < 2 * kPaceXcds; ++x)
+        __hip_atomic_store(g_rem_pace + x * kPaceStride, 0u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -545,6 +600,15 @@ int env_or(const char* name, int dflt);
 int rem_sync_blocks(int lpe) {
   static const int w4 = env_or("APPNP_REM_SYNC_W4", 0), w8 = env_or("APPNP_REM_SYNC_W8", 32),
                    w16 = env_or("APPNP_REM_SYNC_W16", 32);
+  return lpe == 1 ? w4 : lpe == 2 ? w8 : w16;
+}
+
+// XCD-wide pacing at the barriers of the pass of width 4 lpe (0: none; p > 0: a workgroup waits
+// at each barrier until its XCD's workgroups have finished all but p - 1 of its barrier periods;
+// VERDICT r4 #2).  APPNP_REM_PACE_W4 / _W8 / _W16 (measurement; off by default).
+int rem_pace(int lpe) {
+  static const int w4 = env_or("APPNP_REM_PACE_W4", 0), w8 = env_or("APPNP_REM_PACE_W8", 0),
+                   w16 = env_or("APPNP_REM_PACE_W16", 0);
   return lpe == 1 ? w4 : lpe == 2 ? w8 : w16;
 }
 
@@ -731,9 +795,10 @@ hipError_t launch_remainder(const appnp_graph* g, const StepArgs& a_in, int epi,
   if (a.n_rows <= 0) return hipSuccess;
   const bool vf = g->rb_val == nullptr;
   const int lpe = g->rb_lpe;
+  const int sync = rem_sync_blocks(lpe);
   RemLayout L{g->rb_off, g->rb_ent, g->rb_val, g->rb_cblk, g->rb_dl, g->rb_dr, g->rb_nb,
               g->rb_br_log2, g->rb_slots, g->rb_rg, g->rb_passes, to_rem ? 1 : 0,
-              rem_sync_blocks(lpe)};
+              sync, sync > 0 ? rem_pace(lpe) : 0};
   const size_t lds = (size_t)kRemWaves * g->rb_rg * lpe * sizeof(f32x4);
   const dim3 grid((unsigned)g->rb_grid), block(kRemThreads);
   if (epi == EPI_BWD)

@@ -40,6 +40,13 @@ def main():
     p.add_argument("--sb-oom-rank", type=int, default=-1,
                    help="this rank's copy fails to build (APPNP_SB_TEST_OOM): the engines must "
                         "agree on whole rows everywhere")
+    p.add_argument("--offset-rank", type=int, default=-1,
+                   help="this rank passes H and Z 4 bytes off 16-B alignment: it must stage them "
+                        "and take the same (split) path as its peers (ADVICE r4)")
+    p.add_argument("--agree-fail", action="store_true",
+                   help="every rank's split agreement fails after its exchange "
+                        "(APPNP_DIST_TEST_AGREE_FAIL): the first call returns the error, later "
+                        "calls return it again without exchanging (the poisoned handle)")
     a = p.parse_args()
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
@@ -70,7 +77,37 @@ def main():
                                   features=F if a.split else None, dtype=dtype)
     g = pdist._DistGraphInfo(C.c_void_p(_lib.load().appnp_dist_graph(runner._h)))
     before = (g.source_block_layout() or {}).get("launches", 0)
-    Z = runner.run(H[runner.lo:runner.hi].contiguous(), K, alpha, p_drop=a.p_drop, seed=5)
+    if a.agree_fail:
+        os.environ["APPNP_DIST_TEST_AGREE_FAIL"] = "1"
+        codes = []
+        for _ in range(2):
+            try:
+                runner.run(H[runner.lo:runner.hi].contiguous(), K, alpha, seed=5)
+                codes.append(0)
+            except _lib.AppnpError as e:
+                codes.append(e.code)
+            codes.append(getattr(runner, "gloo_calls", 0))
+        # [first code, exchanges after it, second code, exchanges after it]: the agreement's one
+        # exchange, then nothing
+        ok = codes == [_lib.APPNP_EDEVICE, 1, _lib.APPNP_EDEVICE, 1]
+        runner.close()
+        print(f"[dist_capi] rank {rank}/{world} poisoned handle codes/exchanges {codes} -> "
+              f"{'OK' if ok else 'FAIL'}", flush=True)
+        flag = torch.tensor([0 if ok else 1], dtype=torch.int64)
+        dist.all_reduce(flag)
+        dist.destroy_process_group()
+        sys.exit(1 if flag.item() else 0)
+    H_rows = H[runner.lo:runner.hi].contiguous()
+    out = None
+    if rank == a.offset_rank and H_rows.numel():
+        # 4 bytes past a 16-B boundary: same leading dimension, misaligned base pointers
+        hbuf = torch.empty(H_rows.numel() + 1, dtype=H_rows.dtype, device=dev)
+        hbuf[1:].copy_(H_rows.reshape(-1))
+        H_rows = hbuf[1:].view(H_rows.shape)
+        out = torch.full(H_rows.numel() + 1, float("nan"), dtype=H_rows.dtype,
+                         device=dev)[1:].view(H_rows.shape)
+        assert H_rows.data_ptr() % 16 and out.data_ptr() % 16
+    Z = runner.run(H_rows, K, alpha, p_drop=a.p_drop, seed=5, out=out)
     torch.cuda.synchronize()
     # the split layout ran: one remainder pass per iteration (appnp_step_split)
     split_ran = (g.source_block_layout() or {}).get("launches", 0) - before == K

@@ -447,6 +447,37 @@ def test_split_decision_is_collective():
     assert proc.stdout.count("split=False") == 2, proc.stdout[-4000:]
 
 
+@pytest.mark.parametrize("extra", [[], ["--overlap"]])
+def test_native_row_engine_misaligned_rank_stays_split(extra):
+    """one rank passes H and Z 4 bytes off 16-B alignment.  It stages them through
+    the workspace and takes the split layout like its peer (round 4 returned APPNP_EINVAL there
+    while the peer waited in the split loop's exchange), and both match appnp_propagate."""
+    env = dict(os.environ, PPNP_DIST_BACKEND="gloo", PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.join(ROOT, "tests", "dist_capi_worker.py"), "--workload", "arxiv-synth",
+           "--features", "100", "--split", "--offset-rank", "1", *extra]
+    proc = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=150)
+    assert proc.returncode == 0, proc.stdout[-3000:] + proc.stderr[-3000:]
+    assert _rank_results(proc.stdout, "dist_capi") == {0: "OK", 1: "OK"}, proc.stdout[-4000:]
+    assert proc.stdout.count("split=True") == 2, proc.stdout[-4000:]
+
+
+def test_native_row_engine_poisoned_after_failed_agreement():
+    """a split agreement that fails after its exchange poisons the handle.  Both
+    ranks inject the failure (APPNP_DIST_TEST_AGREE_FAIL), so neither waits on the other: the
+    first call returns APPNP_EDEVICE after the agreement's one exchange, and the second returns
+    the stored code without exchanging again."""
+    env = dict(os.environ, PPNP_DIST_BACKEND="gloo", PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.join(ROOT, "tests", "dist_capi_worker.py"), "--workload", "arxiv-synth",
+           "--features", "100", "--split", "--agree-fail"]
+    proc = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=150)
+    assert proc.returncode == 0, proc.stdout[-3000:] + proc.stderr[-3000:]
+    assert _rank_results(proc.stdout, "dist_capi") == {0: "OK", 1: "OK"}, proc.stdout[-4000:]
+
+
 @pytest.mark.parametrize("ranks,extra", [(2, []), (2, ["--overlap", "--p-drop", "0.3"]),
                                          (3, ["--overlap"])])
 def test_native_row_engine_split_rows(ranks, extra):
