@@ -104,7 +104,7 @@ def main():
         hbuf = torch.empty(H_rows.numel() + 1, dtype=H_rows.dtype, device=dev)
         hbuf[1:].copy_(H_rows.reshape(-1))
         H_rows = hbuf[1:].view(H_rows.shape)
-        out = torch.full(H_rows.numel() + 1, float("nan"), dtype=H_rows.dtype,
+        out = torch.full((H_rows.numel() + 1,), float("nan"), dtype=H_rows.dtype,
                          device=dev)[1:].view(H_rows.shape)
         assert H_rows.data_ptr() % 16 and out.data_ptr() % 16
     Z = runner.run(H_rows, K, alpha, p_drop=a.p_drop, seed=5, out=out)
