@@ -78,9 +78,11 @@ def main():
             line = line.strip()
             if line.startswith("{") and '"metric"' in line:
                 bench = json.loads(line)
-    # iterations of the profiled command: every propagation of its warm-up and timed steps
-    # (a --cpu-iters 0 run of one GPU or one emulated rank launches nothing else of these kernels)
-    iters = ((bench["warmup"] + bench["steps"]) * bench["config"]["K"]) if bench else 0
+    # iterations of the profiled command: every propagation of its warm-up and timed steps, plus
+    # the one untimed propagation of roofline.kernel_ms (round 5) when the line carries it (a
+    # --cpu-iters 0 run of one GPU or one emulated rank launches nothing else of these kernels)
+    extra = 1 if bench and bench["roofline"].get("kernel_ms") else 0
+    iters = ((bench["warmup"] + bench["steps"] + extra) * bench["config"]["K"]) if bench else 0
     stats = find(a.stats_dir, "kernel_stats.csv")
     shutil.copy(stats, os.path.join(prof, f"{a.tag}_kernel_stats.csv"))
     rows = list(csv.DictReader(open(stats)))
