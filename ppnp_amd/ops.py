@@ -236,15 +236,17 @@ def kernel_times(fn, device, max_launches: int = 1024) -> list[tuple[str, float]
     the launch stream between launches that are stream-ordered anyway; no profiler runs."""
     lib = _lib.load()
     with torch.cuda.device(device):
-        _lib.check("appnp_kernel_timer_begin",
-                   lib.appnp_kernel_timer_begin(int(max_launches), _stream(device)))
+        # fn() runs even if the timer cannot start: at N > 1 it may hold collectives that every
+        # rank must join
+        rc0 = lib.appnp_kernel_timer_begin(int(max_launches), _stream(device))
         try:
             fn()
         finally:
             ms = (C.c_float * max_launches)()
             kinds = (C.c_int * max_launches)()
             n = C.c_int(0)
-            rc = lib.appnp_kernel_timer_end(ms, kinds, max_launches, C.byref(n))
+            rc = lib.appnp_kernel_timer_end(ms, kinds, max_launches, C.byref(n)) if rc0 == 0 else 0
+        _lib.check("appnp_kernel_timer_begin", rc0)
         _lib.check("appnp_kernel_timer_end", rc)
     return [(KERNEL_KINDS.get(kinds[i], str(kinds[i])), float(ms[i]))
             for i in range(min(n.value, max_launches))]
