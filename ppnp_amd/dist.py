@@ -842,10 +842,10 @@ class NativeRowRunner:
         import ctypes as C
 
         self.graph = _DistGraphInfo(C.c_void_p(_lib.load().appnp_dist_graph(self.engine._h)))
-        # the split the engine takes (appnp_dist_propagate: fp32, K >= 2, 16-B aligned H / Z)
+        # the split the engine takes (appnp_dist_propagate: fp32, K >= 2, every rank's copy
+        # built; a misaligned H / Z is staged through the workspace since round 5)
         sp = self.graph.split_layout(self.width) if H.dtype == torch.float32 else None
-        aligned = self.H.stride(0) % 4 == 0 and self.H.data_ptr() % 16 == 0
-        self.remainder_cols = (self.width - sp[0]) if sp and K >= 2 and aligned else 0
+        self.remainder_cols = (self.width - sp[0]) if sp and K >= 2 else 0
 
     @property
     def width(self) -> int:
