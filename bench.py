@@ -181,6 +181,36 @@ def build_info() -> dict:
             "tree_src": here, "match": fields.get("src") == here}
 
 
+def device_info(dev) -> dict:
+    """Which GPU this line ran on (round 5, VERDICT r4 #1: the two timing states switch between
+    boxes): torch's name / arch / uuid / PCI address, and what the amdgpu driver exposes read-only
+    in sysfs for that PCI function -- the HBM vendor, the board's unique id, the VBIOS, and the
+    current memory / fabric / shader clock levels -- so lines in the fast and the slow state can be
+    told apart by hardware.  Fields that cannot be read are null; never raises."""
+    out = {}
+    try:
+        p = torch.cuda.get_device_properties(dev)
+        bdf = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+        out = {"name": p.name, "arch": getattr(p, "gcnArchName", None), "pci": bdf,
+               "uuid": str(getattr(p, "uuid", "")) or None}
+    except Exception as e:  # noqa: BLE001 -- a diagnostic
+        return {"error": f"{type(e).__name__}: {e}"}
+    base = os.path.join("/sys/bus/pci/devices", out["pci"])
+    for key, fname in (("vram_vendor", "mem_info_vram_vendor"), ("unique_id", "unique_id"),
+                       ("vbios", "vbios_version"), ("mclk", "pp_dpm_mclk"),
+                       ("fclk", "pp_dpm_fclk"), ("sclk", "pp_dpm_sclk")):
+        try:
+            with open(os.path.join(base, fname)) as fh:
+                txt = fh.read().strip()
+            if fname.startswith("pp_dpm_"):  # the current level is marked with '*'
+                cur = [ln for ln in txt.splitlines() if ln.rstrip().endswith("*")]
+                txt = cur[0].split(":", 1)[-1].strip(" *") if cur else txt.replace("\n", "; ")
+            out[key] = txt
+        except OSError:
+            out[key] = None
+    return out
+
+
 def traffic_key(workload, dtype_name, kernel_key, f_local, rows, overlap=False) -> str:
     """Key of the PMC traffic of one rank's iteration: what the rank RUNS -- the workload, the
     dtype, the iteration's kernels, its feature slab width and held rows, the local/remote split
@@ -816,6 +846,7 @@ def main(argv=None):
             },
             "roofline": rl,
             "build": binfo,
+            "device": device_info(dev),
         }
 
     stream = torch.cuda.current_stream(dev)

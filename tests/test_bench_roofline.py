@@ -206,3 +206,16 @@ def test_emulated_rank_key_equals_real_rank_key(world):
             assert real == emu, (r, spec, real, emu)
             assert "EMULATED" not in emu and "rows" in emu
             assert (":ov:" in real) == (overlap and spec != "col")
+
+
+def test_device_info_never_raises():
+    """The bench line's ``device`` block is a diagnostic: without a GPU it reports the error
+    instead of raising (on the box: name, PCI address, HBM vendor, clocks from sysfs)."""
+    import torch
+
+    info = bench.device_info(torch.device("cuda", 0))
+    assert isinstance(info, dict)
+    if not torch.cuda.is_available():
+        assert "error" in info
+    else:
+        assert {"name", "pci", "vram_vendor", "mclk"} <= set(info)
