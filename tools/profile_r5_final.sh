@@ -11,6 +11,7 @@ tools/gpu_session.sh \
  "bench_default::300::python bench.py"
 else
 tools/gpu_session.sh \
+ "bench_box::200::python bench.py --cpu-iters 0" \
  "n2_products::600::PPNP_DIST_BACKEND=gloo $R --nproc-per-node 2 --master-port 29526 bench.py --gpus 2 --steps 2 --warmup 1" \
  "n4_products::600::PPNP_DIST_BACKEND=gloo $R --nproc-per-node 4 --master-port 29527 bench.py --gpus 4 --steps 2 --warmup 1"
 fi
