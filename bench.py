@@ -502,6 +502,7 @@ def kernel_split(run, device, K, iteration_ms):
         "sum_of_kernels": total / K if K else total,
         "iteration": iteration_ms,
         "launches": [kind for kind, _ in t],
+        "ms_per_launch": [round(ms, 5) for _, ms in t],
         "source": "appnp_kernel_timer_begin/_end (include/ppnp_amd.h): one untimed propagation "
                   "after the timed region, a HIP event after every launch on its stream; "
                   "main = the SpMM kernel, rem = the remainder pass, copy = the split copy "
