@@ -16,7 +16,8 @@ prints the fastest one whose parity holds.  The candidate without a data-path ex
 column layout) is measured first, and every later candidate runs under a deadline
 (--candidate-timeout): if an exchange stalls, the RCCL communicators are aborted, rank 0
 prints the best line measured so far, and every rank exits -- the scaling run always gets a
-line unless the exchange-free layout itself fails.
+line unless the exchange-free layout itself fails.  --run-budget bounds the whole run: no
+candidate starts with less than MIN_CANDIDATE_S of it left, and a running one is cut short.
 
 Extra JSON fields:
   roofline      HBM roofline of the iteration's kernels on one rank: algorithmic bytes per
@@ -27,7 +28,10 @@ Extra JSON fields:
                 fastest measured random-line rate, the remainder pass's count floor;
                 exchange at the xGMI link peak).  ``traffic``: committed PMC bytes of the
                 rank's kernels.  ``box_line_rate``: this GPU's random-line rate, probed right
-                before the timed region.
+                before the timed region.  ``kernel_ms``: every launch of one untimed
+                propagation right after the timed region, timed by the library's per-launch
+                timer (appnp_kernel_timer_*), per kind and per launch.
+  device        the GPU the line ran on: PCI address, HBM vendor, board id, VBIOS, clocks.
   cpu_baseline  the oracle's torch.sparse.mm CPU loop (oracle/ppnp_oracle.py) on the same
                 graph and H, all K iterations, rank 0 (N = 1: after the timed region; N > 1:
                 once, before the first candidate).
