@@ -71,6 +71,59 @@ __global__ __launch_bounds__(256) void k_lines(const f4* __restrict__ table, uin
   if (acc.x == 1.2345e-30f) sink[0] = acc.y;
 }
 
+// gather `requests` random ROWS of 3 lines (384 B, the main SpMM's 96 columns) from
+// table[n_rows * 24] (f4 units): 32 lanes per row, 24 active (the SpMM's lane mapping), 2 rows
+// per wave instruction, U rows in flight per sub-group; all XCDs
+template <int U>
+__global__ __launch_bounds__(256) void k_rows3(const f4* __restrict__ table, uint32_t n_rows,
+                                               int64_t requests, uint64_t seed,
+                                               unsigned long long* ctr, float* sink) {
+  __shared__ long long chunk;
+  const int lane = threadIdx.x & 63, sub = lane / 32, gl = lane % 32, w = threadIdx.x >> 6;
+  f4 acc = {0, 0, 0, 0};
+  for (;;) {
+    if (threadIdx.x == 0) chunk = (long long)atomicAdd(ctr, 1ull);
+    __syncthreads();
+    const int64_t c0 = chunk * (kChunk / 4);
+    __syncthreads();
+    if (c0 >= requests) break;
+    for (int64_t base = c0 + w * 2 * U; base < c0 + kChunk / 4 && base < requests;
+         base += 4 * 2 * U) {
+      f4 z[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint64_t e = (uint64_t)(base + u * 2 + sub);
+        const uint32_t h = (uint32_t)mix(seed + e);
+        const uint32_t r = __umulhi(h, n_rows);
+        z[u] = gl < 24 ? table[(int64_t)r * 24 + gl] : f4{0, 0, 0, 0};
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc += z[u];
+    }
+  }
+  if (acc.x == 1.2345e-30f) sink[0] = acc.y;
+}
+
+template <int U>
+void run_rows3(const f4* table, uint32_t n_rows, unsigned long long* ctr, float* sink,
+               hipStream_t s, hipEvent_t a, hipEvent_t b) {
+  const int64_t rows = 1ll << 27;  // 3 x 2^27 lines
+  for (int rep = 0; rep < 2; ++rep) {
+    CHECK(hipMemset(ctr, 0, sizeof(unsigned long long)));
+    CHECK(hipDeviceSynchronize());
+    CHECK(hipEventRecord(a, s));
+    hipLaunchKernelGGL(k_rows3<U>, dim3(2048), dim3(256), 0, s, table, n_rows, rows,
+                       99ull + rep, ctr, sink);
+    CHECK(hipEventRecord(b, s));
+    CHECK(hipDeviceSynchronize());
+    float ms = 0;
+    CHECK(hipEventElapsedTime(&ms, a, b));
+    if (rep == 1)
+      printf("384-B rows, %d rows in flight per sub-group %9.3f ms %8.2f G lines/s\n", U, ms,
+             3.0 * rows / (ms * 1e-3) / 1e9);
+  }
+}
+
 int main(int argc, char** argv) {
   const int64_t table_mb = argc > 1 ? atoll(argv[1]) : 940;
   const uint32_t n_lines = (uint32_t)(table_mb * (1 << 20) / 128);
@@ -133,5 +186,11 @@ int main(int argc, char** argv) {
                k.mask ? requests / (ms * 1e-3) / 1e9 : 0.0, k.l2mask ? ms2 : 0.0);
     }
   }
+  // the main SpMM's row shape: 3 consecutive lines per random row, 24 of 32 lanes
+  const uint32_t n_rows = (uint32_t)((size_t)n_lines * 128 / 384);
+  run_rows3<1>(table, n_rows, ctr, sink, s0, a, b);
+  run_rows3<2>(table, n_rows, ctr, sink, s0, a, b);
+  run_rows3<4>(table, n_rows, ctr, sink, s0, a, b);
+  run_rows3<8>(table, n_rows, ctr, sink, s0, a, b);
   return 0;
 }
