@@ -390,9 +390,10 @@ int appnp_line_rate_probe(const void* table, int64_t table_bytes, int64_t lines,
 /*
  * Measurement aid (no counterpart in the reference): the device time of every launch of the
  * calls made between appnp_kernel_timer_begin and appnp_kernel_timer_end on the calling thread.
- * begin records a start event on `stream`; while the timer is on, appnp_propagate,
- * appnp_propagate_bwd, appnp_step, appnp_step_split and appnp_split_copy (and so
- * appnp_dist_propagate) record a timing event after each launch, tagged with its kind.  The
+ * While the timer is on, appnp_propagate, appnp_propagate_bwd, appnp_step, appnp_step_split
+ * and appnp_split_copy (and so appnp_dist_propagate) record a timing event after each launch,
+ * tagged with its kind, and the first of them a start event right before its first launch (so
+ * no host time before the call is counted; `stream` of begin is unused).  The
  * events sit between launches that are stream-ordered anyway, so the launches run as they
  * would without them, but a call timed this way is not graph-capturable.  end waits for the
  * events and writes, for the first min(n, max) launches, kinds[i] (APPNP_KT_*) and ms[i]: the

@@ -116,6 +116,7 @@ hipError_t launch_scale_rows(int dtype, const void* src, int64_t ld_src, void* d
 // appnp_capi.hip: the per-launch timer of appnp_kernel_timer_begin / _end.  While it is on
 // (on this thread), every launch of the propagation entry points is followed by a timing event
 // on its stream, tagged with the launch's kind (APPNP_KT_*).  Off: one thread-local load.
+void ktimer_start(hipStream_t s);  // the start event, right before a timed call's first launch
 void ktimer_mark(hipStream_t s, int kind);
 
 // Leading dimension of the internal ping-pong buffers.  A random row gather costs 128-B line
