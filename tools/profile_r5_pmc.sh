@@ -35,5 +35,5 @@ else
   add row8 --layout row --overlap --emulate 8:0
 fi
 T="python -u -m pytest -x -q --timeout 150 --timeout-method thread"
-[ "${1:-a}" = a ] && specs=("dist_new::400::$T tests/test_gpu_configs.py -k 'misaligned or poisoned'" "${specs[@]}")
+[ "${1:-a}" = a ] && specs=("probe_tests::300::$T tests/test_gpu_probe.py" "${specs[@]}")
 tools/gpu_session.sh "${specs[@]}"
