@@ -219,3 +219,24 @@ def test_device_info_never_raises():
         assert "error" in info
     else:
         assert {"name", "pci", "vram_vendor", "mclk"} <= set(info)
+
+
+def test_kernel_split_summarises_launches(monkeypatch):
+    """roofline.kernel_ms from the per-launch list (ppnp_amd.ops.kernel_times stubbed: no GPU):
+    per-kind mean / min / max, the per-iteration sum beside the timed iteration, and the
+    per-launch list; an empty list (a captured plan records no launches) stays well-formed."""
+    import torch
+
+    import ppnp_amd.ops as ops
+
+    seq = [("copy", 0.4)] + [("step", 7.4), ("rem", 0.77)] * 10
+    monkeypatch.setattr(ops, "kernel_times", lambda fn, device: seq)
+    monkeypatch.setattr(torch.cuda, "synchronize", lambda *a, **k: None)
+    k = bench.kernel_split(lambda: None, "cuda:0", 10, 8.2)
+    assert k["main"]["launches"] == 10 and k["main"]["mean"] == pytest.approx(7.4)
+    assert k["rem"]["mean"] == pytest.approx(0.77) and k["copy"]["launches"] == 1
+    assert k["sum_of_kernels"] == pytest.approx((0.4 + 10 * (7.4 + 0.77)) / 10)
+    assert k["iteration"] == 8.2 and len(k["ms_per_launch"]) == 21
+    monkeypatch.setattr(ops, "kernel_times", lambda fn, device: [])
+    k = bench.kernel_split(lambda: None, "cuda:0", 10, 8.2)
+    assert k["main"] is None and k["sum_of_kernels"] == 0.0 and k["launches"] == []
