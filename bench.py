@@ -554,13 +554,17 @@ def _abort_rccl():
 
 def process_age_s() -> float:
     """Seconds since this process started (the run budget's clock): the kernel's start time of
-    the process, so the first ``import torch`` of a fresh box (1-2 minutes) counts too."""
+    the process, so the first ``import torch`` of a fresh box (1-2 minutes) counts too.  A start
+    time that puts the process more than 15 minutes before this module's import (a clock the
+    container does not share) is not trusted: then the import is the start, plus 2 minutes."""
+    since_import = time.monotonic() - _T_IMPORT
     try:
         import psutil
 
-        return max(0.0, time.time() - psutil.Process().create_time())
-    except Exception:  # noqa: BLE001 -- psutil missing: count from this module's import
-        return time.monotonic() - _T_IMPORT
+        age = time.time() - psutil.Process().create_time()
+    except Exception:  # noqa: BLE001 -- psutil missing
+        return since_import
+    return age if since_import <= age <= since_import + 900.0 else since_import + 120.0
 
 
 _T_IMPORT = time.monotonic()

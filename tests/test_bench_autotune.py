@@ -181,3 +181,18 @@ def test_run_budget_cuts_a_running_candidate_short(tmp_path):
 
 if __name__ == "__main__":
     pytest.main([__file__, "-q"])
+
+
+def test_process_age_distrusts_a_foreign_clock(monkeypatch):
+    """The run budget's clock: the process's start time, unless it lies before this module's
+    import by more than 15 minutes (a clock the container does not share)."""
+    import types
+
+    import bench
+
+    assert 0.0 <= bench.process_age_s() < 900.0
+    fake = types.SimpleNamespace(Process=lambda: types.SimpleNamespace(
+        create_time=lambda: time.time() - 10 * 3600))
+    monkeypatch.setitem(__import__("sys").modules, "psutil", fake)
+    age = bench.process_age_s()
+    assert age < 900.0
