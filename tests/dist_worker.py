@@ -46,6 +46,10 @@ def main():
                    help="compare with the oracle's float64 torch.sparse CPU loop over the device "
                         "A_hat of a whole-graph build (products scale: tests/test_gpu_configs.py "
                         "pins that A_hat to calc_a_hat entry by entry)")
+    p.add_argument("--oracle-rank0", action="store_true",
+                   help="with --oracle-torch: rank 0 alone runs the oracle and sends every rank "
+                        "its block (gloo point to point), instead of every rank running it -- "
+                        "8 products-scale fp64 oracles would not fit the box's CPU share")
     p.add_argument("--expect-split", type=int, default=None,
                    help="fail unless the rank's remainder columns (split rows) equal this")
     p.add_argument("--sb-oom-rank", type=int, default=-1,
@@ -83,36 +87,35 @@ def main():
                                            p_drop=a.p_drop, seed=5, exchange=a.exchange)
     Z = runner.run()
     torch.cuda.synchronize()
-    if a.oracle_torch:
-        from oracle import ppnp_oracle as O
-
-        G = ppnp_amd.Graph.from_csr(indptr, indices, None, a.n, device=dev)
-        rp, col, val, _ = G.csr()
-        A = torch.sparse_csr_tensor(rp.cpu().long(), col.cpu().long(), val.cpu().double(),
-                                    size=(a.n, a.n))
-        G.close()
-        del rp, col, val
-        torch.set_num_threads(max(1, min(8, len(os.sched_getaffinity(0)))))
-        ref = O.appnp_propagate_torch_cpu(A, H.cpu().double(), a.K, a.alpha)
-        del A
-    elif a.oracle:
-        import numpy as np
-        import scipy.sparse as sp
-
-        from oracle import ppnp_oracle as O
-
-        adj = sp.csr_matrix((np.ones(indices.numel(), dtype=np.float32), indices.cpu().numpy(),
-                             indptr.cpu().numpy()), shape=(a.n, a.n))
-        ref = torch.from_numpy(O.appnp_propagate(O.calc_a_hat(adj, "sym"),
-                                                 H.double().cpu().numpy(), a.K, a.alpha,
-                                                 p_drop=a.p_drop, seed=5)).to(dev)
+    if a.oracle_torch and a.oracle_rank0:
+        if dist.get_backend() != "gloo":
+            raise SystemExit("--oracle-rank0 sends the blocks over gloo")
+        ref = _torch_oracle(a, indptr, indices, H, dev, threads=16) if rank == 0 else None
+        block, ref_max = _send_blocks(ref, (runner.lo, runner.hi, runner.f_lo, runner.f_hi),
+                                      rank, world)
+        del ref
     else:
-        G = ppnp_amd.Graph.from_csr(indptr, indices, None, a.n, device=dev)
-        ref = ppnp_amd.propagate_forward(G, H, a.K, a.alpha, p_drop=a.p_drop, seed=5)
-    block = ref[runner.lo:runner.hi, runner.f_lo:runner.f_hi]
+        if a.oracle_torch:
+            ref = _torch_oracle(a, indptr, indices, H, dev, threads=8)
+        elif a.oracle:
+            import numpy as np
+            import scipy.sparse as sp
+
+            from oracle import ppnp_oracle as O
+
+            adj = sp.csr_matrix((np.ones(indices.numel(), dtype=np.float32),
+                                 indices.cpu().numpy(), indptr.cpu().numpy()), shape=(a.n, a.n))
+            ref = torch.from_numpy(O.appnp_propagate(O.calc_a_hat(adj, "sym"),
+                                                     H.double().cpu().numpy(), a.K, a.alpha,
+                                                     p_drop=a.p_drop, seed=5)).to(dev)
+        else:
+            G = ppnp_amd.Graph.from_csr(indptr, indices, None, a.n, device=dev)
+            ref = ppnp_amd.propagate_forward(G, H, a.K, a.alpha, p_drop=a.p_drop, seed=5)
+        block = ref[runner.lo:runner.hi, runner.f_lo:runner.f_hi]
+        ref_max = ref.abs().max().item()
     got = Z if Z.device == block.device else Z.cpu()
     err = (got.double() - block.double()).abs().max().item() if block.numel() else 0.0
-    tol = 1e-5 * ref.abs().max().item() + 1e-6
+    tol = 1e-5 * ref_max + 1e-6
     ok = err <= tol
     if a.expect_split is not None:
         ok = ok and runner.remainder_cols == a.expect_split
@@ -129,6 +132,40 @@ def main():
     dist.all_reduce(flag)
     dist.destroy_process_group()
     sys.exit(1 if flag.item() else 0)
+
+
+def _torch_oracle(a, indptr, indices, H, dev, threads):
+    """The oracle's float64 torch.sparse CPU loop over the device A_hat of a whole-graph build."""
+    import ppnp_amd
+    from oracle import ppnp_oracle as O
+
+    G = ppnp_amd.Graph.from_csr(indptr, indices, None, a.n, device=dev)
+    rp, col, val, _ = G.csr()
+    A = torch.sparse_csr_tensor(rp.cpu().long(), col.cpu().long(), val.cpu().double(),
+                                size=(a.n, a.n))
+    G.close()
+    del rp, col, val
+    torch.set_num_threads(max(1, min(threads, len(os.sched_getaffinity(0)))))
+    return O.appnp_propagate_torch_cpu(A, H.cpu().double(), a.K, a.alpha)
+
+
+def _send_blocks(ref, mine, rank, world):
+    """Rank 0 holds the whole Z_K (ref) and sends every other rank its (rows, columns) block,
+    point to point over gloo.  Returns (this rank's block, max |Z_K| over the whole matrix)."""
+    blocks = [None] * world
+    dist.all_gather_object(blocks, mine)
+    if rank == 0:
+        for r in range(1, world):
+            lo, hi, f_lo, f_hi = blocks[r]
+            dist.send(ref[lo:hi, f_lo:f_hi].contiguous(), dst=r)
+        block = ref[mine[0]:mine[1], mine[2]:mine[3]].clone()
+        m = torch.tensor([ref.abs().max().item()], dtype=torch.float64)
+    else:
+        block = torch.empty((mine[1] - mine[0], mine[3] - mine[2]), dtype=torch.float64)
+        dist.recv(block, src=0)
+        m = torch.zeros(1, dtype=torch.float64)
+    dist.all_reduce(m, op=dist.ReduceOp.MAX)  # the tolerance scales with the whole Z_K
+    return block, m.item()
 
 
 if __name__ == "__main__":

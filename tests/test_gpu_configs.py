@@ -14,7 +14,9 @@ compares the WHOLE Z_K with an oracle computed on the CPU from the same A and H:
   graph of the same size (hub rows);
 * config 4 row-partitioned over 2 and 4 ranks sharing the one GPU (gloo exchange, with and
   without the overlapped local/remote split), each rank against the float64 oracle:
-  tests/dist_worker.py launched by torch.distributed.run as fresh child processes.
+  tests/dist_worker.py launched by torch.distributed.run as fresh child processes;
+* config 5 row-partitioned: products-synth over 2 ranks (K = 2) and over the north_star's 8
+  ranks (all K = 10 iterations, rank 0's float64 oracle sent to every rank).
 """
 
 import os
@@ -404,6 +406,26 @@ def test_products_row_partition_matches_oracle(extra):
     assert res == {0: "OK", 1: "OK"}, proc.stdout[-4000:]
 
 
+def test_products_eight_rank_row_partition_k10_matches_oracle():
+    """the north_star's own shape -- products-synth row-partitioned over 8
+    ranks (time-sliced on the one GPU, gloo exchange staged through host memory), all K = 10
+    iterations, overlapped local/remote split, every rank on the split rows of its held rows.
+    Rank 0 runs the float64 torch.sparse oracle once and sends each rank its block; every block
+    of Z_K must match it to 1e-5 of max |Z_K|."""
+    env = dict(os.environ, PPNP_DIST_BACKEND="gloo", PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=8",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.join(ROOT, "tests", "dist_worker.py"), "--layout", "row", "--workload",
+           "products-synth", "--oracle-torch", "--oracle-rank0", "--expect-split", "4",
+           "--overlap"]
+    proc = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=400)
+    assert proc.returncode == 0, proc.stdout[-3000:] + proc.stderr[-3000:]
+    res = _rank_results(proc.stdout, "dist_worker")
+    assert res == {r: "OK" for r in range(8)}, proc.stdout[-4000:]
+    lines = [l for l in proc.stdout.splitlines() if l.startswith("[dist_worker]")]
+    assert all("rows=8, cols=1" in l and "overlap=True" in l for l in lines), lines
+
+
 @pytest.mark.parametrize("f,exchange,split", [(72, "multipath", 4), (72, "group", 4),
                                               (73, "multipath", 0)])
 def test_two_d_layout_split_rows_match_oracle(f, exchange, split):
@@ -494,3 +516,22 @@ def test_native_row_engine_split_rows(ranks, extra):
     res = _rank_results(proc.stdout, "dist_capi")
     assert res == {r: "OK" for r in range(ranks)}, proc.stdout[-4000:]
     assert proc.stdout.count("split=True") == ranks, proc.stdout[-4000:]
+
+
+def test_native_row_engine_products_eight_ranks():
+    """The library's own row loop (appnp_dist_propagate, the bench's rows8xcols1-overlap-native
+    candidate) at the north_star's shape: products-synth over 8 ranks sharing the GPU, all
+    K = 10 iterations, overlapped, every rank on the split layout of its held rows (3 gathered
+    lines + the remainder pass, both parts exchanged through the callback), against the
+    single-GPU appnp_propagate, which test_products_k10_matches_oracle pins to the float64
+    oracle."""
+    env = dict(os.environ, PPNP_DIST_BACKEND="gloo", PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=8",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.join(ROOT, "tests", "dist_capi_worker.py"), "--workload", "products-synth",
+           "--split", "--overlap"]
+    proc = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert proc.returncode == 0, proc.stdout[-3000:] + proc.stderr[-3000:]
+    res = _rank_results(proc.stdout, "dist_capi")
+    assert res == {r: "OK" for r in range(8)}, proc.stdout[-4000:]
+    assert proc.stdout.count("split=True") == 8, proc.stdout[-4000:]
