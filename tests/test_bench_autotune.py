@@ -16,7 +16,6 @@ No GPU, no HIP library.
 
 import json
 import os
-import socket
 import time
 
 import pytest
@@ -24,18 +23,19 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+def _rendezvous():
+    """A file:// init method, fresh per run: no TCP port to race for between picking it and
+    the store binding it (torch's FileStore removes the file when the last rank is done)."""
+    import tempfile
+    import uuid
+
+    d = os.path.join(tempfile.gettempdir(), "ppnp_rdv")
+    os.makedirs(d, exist_ok=True)
+    return "file://" + os.path.join(d, uuid.uuid4().hex)
 
 
-def _worker(rank, world, port, plan, out, timeout_s, budget_s=0.0):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+def _worker(rank, world, init, plan, out, timeout_s, budget_s=0.0):
+    dist.init_process_group("gloo", init_method=init, rank=rank, world_size=world)
     import bench
 
     bench.MIN_CANDIDATE_S = 0.5  # the budget's floor, scaled to the stubs' seconds
@@ -80,8 +80,14 @@ def _worker(rank, world, port, plan, out, timeout_s, budget_s=0.0):
 
 def _run(plan, tmp_path, world=2, timeout_s=60.0, budget_s=0.0):
     out = str(tmp_path / "line")
-    mp.start_processes(_worker, args=(world, _free_port(), plan, out, timeout_s, budget_s),
-                       nprocs=world, join=True, start_method="spawn")
+    init = _rendezvous()
+    try:
+        mp.start_processes(_worker, args=(world, init, plan, out, timeout_s, budget_s),
+                           nprocs=world, join=True, start_method="spawn")
+    finally:
+        # a rank that leaves without destroying its group (the deadline paths) keeps the file
+        if os.path.exists(init[len("file://"):]):
+            os.remove(init[len("file://"):])
     res = {}
     for r in range(world):
         if os.path.exists(f"{out}.{r}"):

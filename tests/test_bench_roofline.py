@@ -154,13 +154,11 @@ def _noop_step(runner, src, out_rows, k, part):
     pass
 
 
-def _key_worker(rank, world, port, q):
+def _key_worker(rank, world, init, q):
     import torch
     import torch.distributed as dist
 
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=init, rank=rank, world_size=world)
     try:
         from ppnp_amd.dist import Layout, NullComm, PartitionedAPPNP
 
@@ -188,17 +186,17 @@ def test_emulated_rank_key_equals_real_rank_key(world):
     rank r of a real P-rank run (a gloo process group here) and its single-GPU emulation
     (rank=r, world=P, NullComm: what --emulate P:r builds) look up the same committed PMC
     entry."""
-    import socket
+    import tempfile
+    import uuid
 
     import torch.multiprocessing as mp
 
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
+    d = os.path.join(tempfile.gettempdir(), "ppnp_rdv")  # file:// rendezvous: no port race
+    os.makedirs(d, exist_ok=True)
+    init = "file://" + os.path.join(d, uuid.uuid4().hex)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    mp.start_processes(_key_worker, args=(world, port, q), nprocs=world, join=True,
+    mp.start_processes(_key_worker, args=(world, init, q), nprocs=world, join=True,
                        start_method="spawn")
     res = dict(q.get() for _ in range(world))
     for r, rows in res.items():

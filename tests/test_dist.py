@@ -7,7 +7,6 @@ overlap mode, for row, column and 2-D layouts.
 """
 
 import os
-import socket
 
 import numpy as np
 import pytest
@@ -53,10 +52,8 @@ def _oracle_step(runner, src, out_rows, k, part):
         out_rows[:, :w] = torch.from_numpy(a * (g.rows_csr @ Zin) + runner.alpha * H).float()
 
 
-def _worker(rank, world, port, layout_spec, overlap, q, exchange="multipath", f=F):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+def _worker(rank, world, init, layout_spec, overlap, q, exchange="multipath", f=F):
+    dist.init_process_group("gloo", init_method=init, rank=rank, world_size=world)
     try:
         from ppnp_amd.dist import Layout, PartitionedAPPNP
 
@@ -77,12 +74,15 @@ def _worker(rank, world, port, layout_spec, overlap, q, exchange="multipath", f=
         dist.destroy_process_group()
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+def _rendezvous():
+    """A file:// init method, fresh per run: no TCP port to race for between picking it and
+    the store binding it (torch's FileStore removes the file when the last rank is done)."""
+    import tempfile
+    import uuid
+
+    d = os.path.join(tempfile.gettempdir(), "ppnp_rdv")
+    os.makedirs(d, exist_ok=True)
+    return "file://" + os.path.join(d, uuid.uuid4().hex)
 
 
 @pytest.mark.parametrize("world,layout,overlap,exchange,f", [
@@ -102,7 +102,7 @@ def _free_port():
 def test_partitioned_matches_oracle(world, layout, overlap, exchange, f):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    mp.start_processes(_worker, args=(world, _free_port(), layout, overlap, q, exchange, f),
+    mp.start_processes(_worker, args=(world, _rendezvous(), layout, overlap, q, exchange, f),
                        nprocs=world, join=True, start_method="spawn")
     res = sorted(q.get() for _ in range(world))
     covered = np.zeros((N, f), dtype=bool)
@@ -251,10 +251,8 @@ def test_multipath_plan(spec, world):
         assert dict(got) == {a: shard for a in group if a != r}
 
 
-def _agree_worker(rank, world, port, splits, q):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+def _agree_worker(rank, world, init, splits, q):
+    dist.init_process_group("gloo", init_method=init, rank=rank, world_size=world)
     try:
         from ppnp_amd.dist import agree_split
 
@@ -279,7 +277,7 @@ def test_split_agreement_needs_equal_parts(splits, agreed):
     the parts are exchanged between column groups as equal-size messages."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    mp.start_processes(_agree_worker, args=(4, _free_port(), splits, q), nprocs=4, join=True,
+    mp.start_processes(_agree_worker, args=(4, _rendezvous(), splits, q), nprocs=4, join=True,
                        start_method="spawn")
     res = dict(q.get() for _ in range(4))
     assert all(v == agreed for v in res.values()), res

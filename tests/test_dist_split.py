@@ -12,7 +12,6 @@ last iteration into the held rows of Z, and uneven shards.
 """
 
 import os
-import socket
 
 import numpy as np
 import pytest
@@ -80,10 +79,8 @@ def _step_split(g, part, zin_main, zin_rem, H, f, k, alpha, out_main=None, out_r
         out_rem[g.row_lo:g.row_hi, :r] = torch.from_numpy(remv).float()
 
 
-def _worker(rank, world, port, overlap, q):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+def _worker(rank, world, init, overlap, q):
+    dist.init_process_group("gloo", init_method=init, rank=rank, world_size=world)
     try:
         from ppnp_amd import dist as pdist
         from ppnp_amd import ops
@@ -112,19 +109,22 @@ def _worker(rank, world, port, overlap, q):
         dist.destroy_process_group()
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+def _rendezvous():
+    """A file:// init method, fresh per run: no TCP port to race for between picking it and
+    the store binding it (torch's FileStore removes the file when the last rank is done)."""
+    import tempfile
+    import uuid
+
+    d = os.path.join(tempfile.gettempdir(), "ppnp_rdv")
+    os.makedirs(d, exist_ok=True)
+    return "file://" + os.path.join(d, uuid.uuid4().hex)
 
 
 @pytest.mark.parametrize("world,overlap", [(2, False), (2, True), (3, True)])
 def test_row_split_loop_matches_oracle(world, overlap):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    mp.start_processes(_worker, args=(world, _free_port(), overlap, q), nprocs=world, join=True,
+    mp.start_processes(_worker, args=(world, _rendezvous(), overlap, q), nprocs=world, join=True,
                        start_method="spawn")
     res = sorted(q.get() for _ in range(world))
     for rank, err, events in res:
