@@ -72,11 +72,11 @@ XGMI_IN_GBS = 7 * 76.8
 #   * requests: one L2 request per nonzero (an entry's 16 LPE bytes lie in one line) at the rate
 #     of the W4 pass with every gather forced to an L2-resident row: 0.665 ms for products-synth's
 #     126,165,965 nonzeros, entry stream included = 189.7 G requests/s.
-# Row passes: ceil(rows / (CUs x 16 waves x 640 / LPE rows)), as graph_build_source_blocks has it.
+# Row passes and direct rows: rem_row_layout, as graph_build_source_blocks has them.
 REM_L2_REQ_RATE = 126_165_965 / 0.665e-3 / 1e9
 REM_L2_REQ_SOURCE = ("DESIGN.md 4.2: the W4 pass with every gather an L2 hit, 0.665 ms for "
                      "126.2 M nonzeros")
-XCDS, CUS, REM_WAVES, REM_ROWS_LPE1 = 8, 256, 16, 640
+XCDS, CUS, REM_WAVES, REM_LDS_BYTES = 8, 256, 16, 160 * 1024
 # N > 1: the whole run's wall budget, below the driver's 600 s bench timeout with
 # room for the launcher, the first `import torch` of a fresh box and the teardown; a candidate
 # is not started with less than MIN_CANDIDATE_S of it left
@@ -176,13 +176,21 @@ def build_info() -> dict:
 
     here = src_digest()
     try:
-        info = _lib.load().appnp_build_info().decode()
+        lib = _lib.load()
+        info = lib.appnp_build_info().decode()
+        active = lib.appnp_tuning_overrides().decode()
+        names = lib.appnp_tuning_names().decode().split(";")
     except Exception as e:  # noqa: BLE001 -- provenance is reported, never fatal to the line
         return {"library": _lib.LIB_PATH, "info": f"{type(e).__name__}: {e}",
-                "library_src": None, "tree_src": here, "match": False}
+                "library_src": None, "tree_src": here, "match": False, "overrides": None}
     fields = dict(kv.split("=", 1) for kv in info.split(";") if "=" in kv)
+    # tuning overrides in effect (APPNP_TUNING=1), and any set but ignored without it
+    # (a stray variable must not change kernels silently)
+    overrides = dict(kv.split("=", 1) for kv in active.split(";") if "=" in kv)
+    ignored = sorted(k for k in names if os.environ.get(k) and k not in overrides)
     return {"library": _lib.LIB_PATH, "info": info, "library_src": fields.get("src"),
-            "tree_src": here, "match": fields.get("src") == here}
+            "tree_src": here, "match": fields.get("src") == here,
+            "overrides": overrides or None, "overrides_ignored": ignored or None}
 
 
 def device_info(dev) -> dict:
@@ -301,11 +309,15 @@ def kernel_plan(F_local, K, remainder_cols, sb):
         return ("k_step (one fused SpMM launch per iteration)", "k_step", F_local, 0, 1)
     fs = F_local - r
     lpe = sb["width"] // 4
-    rem = f"k_rem_persist<W{sb['width']}{',vf' if sb['value_free'] else ''}>"
+    cols = sb.get("cols", sb["width"])
+    rem = (f"k_rem_persist<W{sb['width']}{',vf' if sb['value_free'] else ''}"
+           f"{f',c{cols}' if cols < sb['width'] else ''}>")
     if not fs:
+        direct = sb.get("direct_rows", 0)
         return (f"{rem} on all {F_local} columns (narrow rows: one persistent L2-blocked launch "
-                f"per iteration, {sb['row_passes']} row passes)", f"{rem}[0,{F_local})", 0, r,
-                lpe)
+                f"per iteration, {sb['row_passes']} row passes"
+                + (f", {direct} rows gathered directly" if direct else "") + ")",
+                f"{rem}[0,{F_local})", 0, r, lpe)
     return (f"k_step on columns [0, {fs}) + {rem} on the remainder columns [{fs}, {F_local}) "
             "(one persistent L2-blocked launch) per iteration; times are per iteration",
             f"k_step[0,{fs})+{rem}[{fs},{F_local})", fs, r, lpe)
@@ -326,24 +338,44 @@ def rank_traffic_key(workload, dtype_name, runner, K) -> str:
                        bool(getattr(runner, "overlap", False)))
 
 
-def remainder_floor(n, rows, nnz, lpe):
+def rem_row_layout(rows, lpe, cols=None):
+    """(row passes, rows per wave group, direct rows) of the W = 4 lpe remainder pass sized for
+    ``cols`` columns, as graph_build_source_blocks lays it out: a row's sums take 16 B (LPE = 1)
+    or 4 cols B of LDS, 16 waves x 256 CUs hold 160 KiB / (16 x that) rows each per row pass,
+    and when the last pass would hold at most 1/8 of the rows it is dropped and those rows are
+    gathered directly."""
+    cols = 4 * lpe if lpe == 1 or not cols else cols
+    row_bytes = 16 if lpe == 1 else 4 * cols
+    max_rg = REM_LDS_BYTES // (REM_WAVES * row_bytes)
+    cap = CUS * REM_WAVES * max_rg
+    passes = max(1, -(-rows // cap))
+    if passes > 1 and rows - (passes - 1) * cap <= rows // 8:
+        return passes - 1, max_rg, rows - (passes - 1) * cap
+    return passes, max(1, -(-rows // (passes * CUS * REM_WAVES))), 0
+
+
+def remainder_floor(n, rows, nnz, lpe, cols=None):
     """The W = 4 lpe remainder pass's floor from counts (see REM_L2_REQ_RATE): the larger of its
-    compulsory L2 fill (+ entry stream) from beyond L2 and its L2 requests at the all-hit rate."""
-    slot_rows = CUS * REM_WAVES * (REM_ROWS_LPE1 // lpe)
-    passes = max(1, -(-rows // slot_rows))
+    compulsory L2 fill (+ entry stream, + one line request per nonzero of its direct rows) from
+    beyond L2 and its L2 requests at the all-hit rate."""
+    passes, _, direct = rem_row_layout(rows, lpe, cols)
     fill_lines = passes * XCDS * n * 16 * lpe / 128
+    direct_lines = nnz * direct / rows if rows else 0.0
     entry_bytes = 4 * nnz
-    fill_ms = (fill_lines / (GATHER_LINE_CEILING * 1e9) + entry_bytes / (HBM_PEAK_GBS * 1e9)) * 1e3
+    fill_ms = ((fill_lines + direct_lines) / (GATHER_LINE_CEILING * 1e9)
+               + entry_bytes / (HBM_PEAK_GBS * 1e9)) * 1e3
     req_ms = nnz / (REM_L2_REQ_RATE * 1e9) * 1e3
     return {"ms": max(fill_ms, req_ms), "fill_ms": fill_ms, "l2_request_ms": req_ms,
-            "row_passes": passes, "fill_lines": fill_lines,
+            "row_passes": passes, "fill_lines": fill_lines, "direct_rows": direct,
+            "direct_lines": direct_lines,
             "kind": "count floor (not a measured rate): max(row passes x 8 XCDs x table / 128-B "
-                    f"lines at {GATHER_LINE_CEILING} G lines/s + 4 B/entry at the HBM peak, "
-                    f"one L2 request per nonzero at {REM_L2_REQ_RATE:.1f} G/s ({REM_L2_REQ_SOURCE}))"}
+                    f"lines + one line per nonzero of the direct rows at {GATHER_LINE_CEILING} "
+                    "G lines/s + 4 B/entry at the HBM peak, one L2 request per nonzero at "
+                    f"{REM_L2_REQ_RATE:.1f} G/s ({REM_L2_REQ_SOURCE}))"}
 
 
 def roofline(*, n, rows, nnz, F_local, esz, avg_iter_ms, fs, r, lpe, exchange_in_bytes=0,
-             kernel="", kernel_key="", traffic=None):
+             kernel="", kernel_key="", traffic=None, cols=None):
     """The roofline block of one rank.
 
     achieved = B_iter / iteration time with B_iter = 4(rows+1) + 8 nnz + (n + 2 rows) F s: the
@@ -377,7 +409,7 @@ def roofline(*, n, rows, nnz, F_local, esz, avg_iter_ms, fs, r, lpe, exchange_in
         dense = 2 * rows * ld * s
     lines = nnz * lpn + (stream + dense) / 128
     width = 4 * lpe
-    rem = remainder_floor(n, rows, nnz, lpe) if r else None
+    rem = remainder_floor(n, rows, nnz, lpe, cols) if r else None
     rem_ms = rem["ms"] if r else 0.0
     compute_ms = lines / (GATHER_LINE_CEILING * 1e9) * 1e3 + rem_ms
     exchange_ms = exchange_in_bytes / (XGMI_IN_GBS * 1e9) * 1e3
@@ -490,6 +522,10 @@ def kernel_split(run, device, K, iteration_ms):
     except Exception as e:  # noqa: BLE001 -- a diagnostic, not the measurement
         log(f"[bench] kernel split failed: {type(e).__name__}: {e}")
         return None
+    if not t:
+        # a replayed plan (--plan) records nothing: say so instead of empty stats
+        return {"note": "no launches recorded (a captured hipGraph replays without the "
+                        "library's per-launch events)", "iteration": iteration_ms}
     by = {}
     for kind, ms in t:
         by.setdefault(kind, []).append(ms)
@@ -498,19 +534,25 @@ def kernel_split(run, device, K, iteration_ms):
         return ({"mean": sum(v) / len(v), "min": min(v), "max": max(v), "launches": len(v)}
                 if v else None)
 
-    total = sum(ms for _, ms in t)
+    total = sum(ms for kind, ms in t if kind != "xchg")
     return {
-        "main": stats(by.get("step", [])),
+        "main": stats(by.get("step", []) + by.get("local", []) + by.get("remote", [])),
+        "local": stats(by.get("local", [])),
+        "remote": stats(by.get("remote", [])),
         "rem": stats(by.get("rem", [])),
         "copy": stats(by.get("copy", [])),
+        "xchg": stats(by.get("xchg", [])),
         "sum_of_kernels": total / K if K else total,
         "iteration": iteration_ms,
         "launches": [kind for kind, _ in t],
         "ms_per_launch": [round(ms, 5) for _, ms in t],
         "source": "appnp_kernel_timer_begin/_end (include/ppnp_amd.h): one untimed propagation "
-                  "after the timed region, a HIP event after every launch on its stream; "
-                  "main = the SpMM kernel, rem = the remainder pass, copy = the split copy "
-                  "(once per call); sum_of_kernels and iteration are ms per iteration",
+                  "after the timed region, HIP events right before and after every launch on "
+                  "its stream (no wait before a launch is counted in it); main = the SpMM "
+                  "kernel (local + remote halves on a row-partitioned graph), rem = the "
+                  "remainder pass, copy = the split copy (once per call), xchg = the library "
+                  "row loop's exchange calls (not in sum_of_kernels); sum_of_kernels and "
+                  "iteration are ms per iteration",
     }
 
 
@@ -815,10 +857,12 @@ def main(argv=None):
         avg_iter_ms = dev_ms / (args.steps * K)
         desc, kkey, fs, r, lpe = rank_kernel_plan(runner, K)
         tkey = rank_traffic_key(args.workload, dname, runner, K)
+        sb = graph.source_block_layout() if r else None
         rl = roofline(n=n, rows=graph.rows, nnz=graph.nnz_hat, F_local=F_local, esz=esz,
                       avg_iter_ms=avg_iter_ms, fs=fs, r=r, lpe=lpe,
                       exchange_in_bytes=exchange_in, kernel=desc, kernel_key=kkey,
-                      traffic=committed_traffic(tkey))
+                      traffic=committed_traffic(tkey), cols=sb.get("cols") if sb else None)
+        rl["source_blocks"] = sb
         rl["traffic_key"] = tkey
         rl["kernel_ms"] = kernel_split(runner.run, dev, K, avg_iter_ms)
         rl["box_line_rate"] = box["G_lines_s"] if box else None

@@ -41,7 +41,11 @@
 extern "C" {
 #endif
 
-#define PPNP_AMD_ABI_VERSION 1
+/* 2 (round 6): appnp_dist_workspace_bytes reserves staging for a misaligned H / Z (a larger
+ * workspace than version 1 asked for); APPNP_GRAPH_SB_COLS; appnp_graph_source_block_rows;
+ * the per-launch timer brackets each launch (start and end events) and has the kinds
+ * APPNP_KT_LOCAL / _REMOTE / _XCHG; appnp_tuning_overrides / appnp_tuning_names. */
+#define PPNP_AMD_ABI_VERSION 2
 
 typedef struct appnp_graph appnp_graph;
 
@@ -83,6 +87,17 @@ enum appnp_norm { APPNP_NORM_SYM = 0, APPNP_NORM_RW = 1 };
  * launch.  Same memory as APPNP_GRAPH_SOURCE_BLOCKS (segments padded to 32 / 16 entries). */
 #define APPNP_GRAPH_SB_W8 0x400
 #define APPNP_GRAPH_SB_W16 0x800
+
+/* OR into `mode` with APPNP_GRAPH_SB_W8 / _W16: size the remainder pass for c remainder columns
+ * (1 <= c <= the copy's width; 0 or absent: the whole width).  The pass keeps each row's sums
+ * in LDS, 4 c bytes instead of 16 or 32 / 64, so a row pass holds more rows: the 13-column
+ * slabs of F = 100 over 8 column ranks take 3 row passes instead of 4 on products-synth (the
+ * rows the last pass would hold, when they are at most 1/8 of them, are gathered directly from
+ * the CSR instead; appnp_graph_source_block_rows).  Propagations whose remainder is wider than
+ * c gather whole rows.  Ignored for APPNP_GRAPH_SOURCE_BLOCKS (always 4). */
+#define APPNP_GRAPH_SB_COLS_SHIFT 16
+#define APPNP_GRAPH_SB_COLS_MASK (0x1f << APPNP_GRAPH_SB_COLS_SHIFT)
+#define APPNP_GRAPH_SB_COLS(c) (((c) & 0x1f) << APPNP_GRAPH_SB_COLS_SHIFT)
 
 /* storage type of H / Z (accumulation is always fp32) */
 enum appnp_dtype { APPNP_F32 = 0, APPNP_BF16 = 1 };
@@ -210,6 +225,12 @@ int appnp_propagate_remainder_cols(const appnp_graph* g, int64_t f, int dtype, i
  * remainder-pass launches enqueued on this graph so far (which path a propagation took). */
 int appnp_graph_source_block_layout(const appnp_graph* g, int* width, int64_t* entries,
                                     int* value_free, int* row_passes, int64_t* launches);
+
+/* The same copy's row layout: *cols remainder columns its pass holds sums for
+ * (APPNP_GRAPH_SB_COLS; 0 = not built), *rows_per_group rows of one wave's group, and
+ * *direct_rows held rows in no group, gathered straight from the CSR by the pass. */
+int appnp_graph_source_block_rows(const appnp_graph* g, int* cols, int* rows_per_group,
+                                  int64_t* direct_rows);
 
 /*
  * Z = APPNP_K(H):  Z_0 = H;  Z_{k+1} = (1-alpha) (M_k o A_hat) Z_k + alpha H,  k < K.
@@ -391,24 +412,39 @@ int appnp_line_rate_probe(const void* table, int64_t table_bytes, int64_t lines,
  * Measurement aid (no counterpart in the reference): the device time of every launch of the
  * calls made between appnp_kernel_timer_begin and appnp_kernel_timer_end on the calling thread.
  * While the timer is on, appnp_propagate, appnp_propagate_bwd, appnp_step, appnp_step_split
- * and appnp_split_copy (and so appnp_dist_propagate) record a timing event after each launch,
- * tagged with its kind, and the first of them a start event right before its first launch (so
- * no host time before the call is counted; `stream` of begin is unused).  The
- * events sit between launches that are stream-ordered anyway, so the launches run as they
- * would without them, but a call timed this way is not graph-capturable.  end waits for the
- * events and writes, for the first min(n, max) launches, kinds[i] (APPNP_KT_*) and ms[i]: the
- * time from the previous event on the same stream (the start event, or the previous launch) to
- * this launch's end, NaN if there is none.  *n_out = launches recorded; APPNP_ERANGE if more
- * than max_launches were enqueued (the rest were not timed).  bench.py prints the split of one
+ * and appnp_split_copy (and so appnp_dist_propagate) bracket each launch by two timing events on
+ * its stream, one right before and one right after it, tagged with its kind; appnp_dist_propagate
+ * brackets each exchange call the same way (APPNP_KT_XCHG, on the stream it is enqueued on).  So
+ * an interval covers its launch only: a wait for another stream, or host time, before a launch is
+ * never counted in it (`stream` of begin is unused).  The events sit between launches that are
+ * stream-ordered anyway, so the launches run as they would without them, but a call timed this
+ * way is not graph-capturable, and a replayed plan (appnp_plan_launch) records nothing.  end
+ * waits for the events and writes, for the first min(n, max) launches, kinds[i] (APPNP_KT_*) and
+ * ms[i], NaN if the pair cannot be timed.  *n_out = launches recorded; APPNP_ERANGE if more than
+ * max_launches were enqueued (the rest were not timed).  bench.py prints the split of one
  * propagation as roofline.kernel_ms.
  */
 enum appnp_kernel_kind {
-  APPNP_KT_COPY = 1,  /* H (or dZ) into the split layout, or a plain copy / scale of rows */
-  APPNP_KT_STEP = 2,  /* the fused SpMM + AXPBY kernel (whole rows or the main columns)  */
-  APPNP_KT_REM = 3    /* the persistent L2-blocked remainder pass                         */
+  APPNP_KT_COPY = 1,   /* H (or dZ) into the split layout, or a plain copy / scale of rows  */
+  APPNP_KT_STEP = 2,   /* the fused SpMM + AXPBY kernel (whole rows or the main columns)   */
+  APPNP_KT_REM = 3,    /* the persistent L2-blocked remainder pass                          */
+  APPNP_KT_LOCAL = 4,  /* appnp_step(_split) PART_LOCAL: the local-column product           */
+  APPNP_KT_REMOTE = 5, /* appnp_step(_split) PART_REMOTE: the remote columns + epilogue     */
+  APPNP_KT_XCHG = 6    /* appnp_dist_propagate: one call of the exchange (all-gather)       */
 };
 int appnp_kernel_timer_begin(int max_launches, void* stream);
 int appnp_kernel_timer_end(float* ms, int* kinds, int max, int* n_out);
+
+/*
+ * Tuning overrides.  A few environment variables (appnp_tuning_names: ';'-separated) reshape
+ * kernels for the measurement sweeps of tools/ -- vector width, entries in flight, the split
+ * rule, the remainder pass's block size and barriers.  The library reads them only when
+ * APPNP_TUNING=1 is set too; otherwise they are ignored and the measured defaults run.
+ * appnp_tuning_overrides returns the ones in effect in this process ("NAME=value;..."), "" when
+ * none; bench.py prints it as build.overrides.
+ */
+const char* appnp_tuning_overrides(void);
+const char* appnp_tuning_names(void);
 
 #ifdef __cplusplus
 }

@@ -15,6 +15,10 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PPNP_AMD_LIB", os.path.join(_HERE, "libppnp_amd.so"))
+# the same library with the fault-injection hooks of the tests compiled in (make's test target;
+# -DAPPNP_TESTING): tests run it in child processes through PPNP_AMD_LIB
+TEST_LIB_PATH = os.path.join(_HERE, "libppnp_amd_test.so")
+ABI_VERSION = 2  # PPNP_AMD_ABI_VERSION of include/ppnp_amd.h
 
 APPNP_OK = 0
 APPNP_EDEVICE = -5
@@ -28,9 +32,16 @@ GRAPH_TRANSPOSE = 0x100
 GRAPH_SOURCE_BLOCKS = 0x200
 GRAPH_SB_W8 = 0x400  # remainder of up to 8 columns (include/ppnp_amd.h)
 GRAPH_SB_W16 = 0x800  # up to 16
+
+
+def GRAPH_SB_COLS(c: int) -> int:
+    """APPNP_GRAPH_SB_COLS(c): size the W8 / W16 remainder pass for c columns."""
+    return (int(c) & 0x1F) << 16
+
+
 F32, BF16 = 0, 1
 PART_ALL, PART_LOCAL, PART_REMOTE = 0, 1, 2
-KT_COPY, KT_STEP, KT_REM = 1, 2, 3  # appnp_kernel_kind
+KT_COPY, KT_STEP, KT_REM, KT_LOCAL, KT_REMOTE, KT_XCHG = 1, 2, 3, 4, 5, 6  # appnp_kernel_kind
 
 _vp, _i64, _i32, _f32, _u64, _sz = C.c_void_p, C.c_int64, C.c_int, C.c_float, C.c_uint64, C.c_size_t
 
@@ -100,6 +111,10 @@ _SIGS = {
     "appnp_line_rate_probe": (_i32, [_vp, _i64, _i64, _u64, _vp, _vp]),
     "appnp_kernel_timer_begin": (_i32, [_i32, _vp]),
     "appnp_kernel_timer_end": (_i32, [_vp, _vp, _i32, C.POINTER(_i32)]),
+    "appnp_tuning_overrides": (C.c_char_p, []),
+    "appnp_tuning_names": (C.c_char_p, []),
+    "appnp_graph_source_block_rows": (_i32, [_vp, C.POINTER(_i32), C.POINTER(_i32),
+                                             C.POINTER(_i64)]),
     "appnp_step": (
         _i32,
         [_vp, _i32, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _f32,
@@ -147,7 +162,7 @@ def load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.appnp_abi_version() != 1:
+    if lib.appnp_abi_version() != ABI_VERSION:
         raise ImportError("ppnp_amd: ABI version mismatch")
     _lib = lib
     return lib

@@ -7,6 +7,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <new>
+#include <string>
 #include <vector>
 
 #include "../../include/ppnp_amd.h"
@@ -17,55 +18,88 @@ using appnp::StepArgs;
 namespace appnp {
 namespace {
 
-// appnp_kernel_timer_*: one timing event per launch, recorded on the launch's stream
+// appnp_kernel_timer_*: two timing events per launch, recorded on the launch's stream right
+// before and right after it
 struct KTimer {
   bool on = false;
   int dropped = 0;              // launches past the capacity (not timed)
-  std::vector<hipEvent_t> ev;   // ev[0]: the start event; ev[i]: after launch i
-  std::vector<hipStream_t> st;
+  std::vector<hipEvent_t> ev;   // ev[2 i]: before launch i; ev[2 i + 1]: after it
   std::vector<int> kind;
-  int n = 0;                    // events recorded
+  int n = 0;                    // launches recorded
+  bool open = false;            // ev[2 n] recorded, its launch's end not yet
+  bool over = false;            // the launch begun now is past the capacity
+  hipStream_t open_s = nullptr;
 
   void release() {
     for (hipEvent_t e : ev) (void)hipEventDestroy(e);
     ev.clear();
-    st.clear();
     kind.clear();
     n = dropped = 0;
-    on = false;
+    on = open = over = false;
+    open_s = nullptr;
   }
 };
 thread_local KTimer g_ktimer;
 
 }  // namespace
 
-void ktimer_start(hipStream_t s) {
+void ktimer_begin(hipStream_t s) {
   KTimer& t = g_ktimer;
-  if (t.on && t.n == 0 && !t.ev.empty() && hipEventRecord(t.ev[0], s) == hipSuccess) {
-    t.st[0] = s;
-    t.kind[0] = 0;
-    t.n = 1;
+  if (!t.on) return;
+  t.open = false;
+  t.over = 2 * t.n + 1 >= (int)t.ev.size();
+  if (!t.over && hipEventRecord(t.ev[2 * t.n], s) == hipSuccess) {
+    t.open = true;
+    t.open_s = s;
   }
 }
 
 void ktimer_mark(hipStream_t s, int kind) {
   KTimer& t = g_ktimer;
-  if (!t.on || t.n == 0) return;  // no start event yet: not a timed call
-  if (t.n >= (int)t.ev.size() || hipEventRecord(t.ev[t.n], s) != hipSuccess) {
+  if (!t.on) return;
+  if (t.over) {
+    ++t.dropped;
+    t.over = false;
+    return;
+  }
+  if (!t.open || t.open_s != s) return;  // no begin on this stream: not a timed launch
+  t.open = false;
+  if (hipEventRecord(t.ev[2 * t.n + 1], s) != hipSuccess) {
     ++t.dropped;
     return;
   }
-  t.st[t.n] = s;
   t.kind[t.n] = kind;
   ++t.n;
+}
+
+// Every tuning override the library reads (tuning_env).  They change which kernel variant runs
+// or how it is shaped, never results beyond fp32 summation order, and exist for the sweeps of
+// tools/; a product run leaves APPNP_TUNING unset and gets the measured defaults.
+const char* const kTuningNames[] = {
+    "APPNP_SPLIT",       "APPNP_VEC",         "APPNP_WIDE",         "APPNP_UW",
+    "APPNP_UN",          "APPNP_NT",          "APPNP_MAX_BLOCKS",   "APPNP_REM_SYNC_W4",
+    "APPNP_REM_SYNC_W8", "APPNP_REM_SYNC_W16", "APPNP_SB_ROWS",     "APPNP_REM_VF"};
+
+bool tuning_on() {
+  static const bool on = [] {
+    const char* v = getenv("APPNP_TUNING");
+    return v && v[0] == '1' && v[1] == '\0';
+  }();
+  return on;
+}
+
+int tuning_env(const char* name, int dflt) {
+  if (!tuning_on()) return dflt;
+  const char* v = getenv(name);
+  return (v && *v) ? atoi(v) : dflt;
 }
 
 }  // namespace appnp
 
 namespace {
 
+using appnp::ktimer_begin;
 using appnp::ktimer_mark;
-using appnp::ktimer_start;
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
@@ -127,12 +161,13 @@ StepArgs base_args(const appnp_graph* g, int64_t f, float alpha) {
   return a;
 }
 
-constexpr double kSplitMaxNear = 0.5;  // split rows only below this gather locality
+constexpr double kSplitMaxNear = 0.5;
 
-int env_flag(const char* name, int dflt) {
-  const char* v = getenv(name);
-  return (v && *v) ? atoi(v) : dflt;
-}
+// the timer kind of an appnp_step / appnp_step_split launch on `part`
+inline int part_kind(int part) {
+  return part == APPNP_PART_LOCAL ? APPNP_KT_LOCAL
+                                  : part == APPNP_PART_REMOTE ? APPNP_KT_REMOTE : APPNP_KT_STEP;
+}  // split rows only below this gather locality
 
 // Whether every operand allows 16-B vectors: leading dimensions multiples of 4 floats and
 // 16-B aligned base pointers (null pointers ignored).  The split path reads and writes H / Z
@@ -154,16 +189,17 @@ bool vec16(const int64_t* lds, int n_ld, const void* const* ptrs, int n_ptr) {
 // latency-regime graph, F outside [1, 256], operands that do not allow 16-B vectors
 // (``aligned``), or a graph with gather locality.  APPNP_SPLIT=0 disables it (measurement).
 int64_t remainder_cols(const appnp_graph* g, int64_t f, int dtype, bool aligned) {
-  static const int enabled = env_flag("APPNP_SPLIT", 1);
+  static const int enabled = appnp::tuning_env("APPNP_SPLIT", 1);
   if (!enabled || !g->rb_off || dtype != APPNP_F32 || !aligned) return 0;
   if (g->n <= (1 << 16) || f < 1 || f > 256) return 0;
   // graphs with gather locality keep whole rows: their last line is mostly an L2 hit, cheaper
   // than the remainder pass (products-local, ~90 % near entries: 4.0 ms whole rows, 3.7 ms for
   // the 3-line main part alone, 8.5 ms split).  Uniform products-synth: 1.3 % near.
   if (g->near_frac > kSplitMaxNear && enabled != 2) return 0;  // APPNP_SPLIT=2: regardless
-  const int64_t w = 4 * (int64_t)g->rb_lpe;
+  // the pass holds sums for the columns the copy was sized for (APPNP_GRAPH_SB_COLS)
+  const int64_t w = appnp::source_block_cols(g);
   const int64_t r = f > 32 ? f % 32 : f;
-  if (f <= 32 && f > w) return 0;  // one line per row already and too wide for the pass
+  if (f <= 32 && f > w) return 0;  // one line per row already, or too wide for the pass
   // beside a main part, a remainder of 9-16 columns costs as much as its extra line
   // (products-synth F = 47: 4.53 ms split against 4.41 ms whole rows; F = 40 = 32 + 8: 3.68
   // against 4.44 ms; profiles/r2_wide_remainder.txt)
@@ -210,6 +246,7 @@ int propagate_split(const appnp_graph* g, const StepArgs& a0, const void* H, int
   auto rem_of = [&](int i) { return reinterpret_cast<float*>(bufs[i] + main_b); };
   const float* h = static_cast<const float*>(H);
   float* z = static_cast<float*>(Z);
+  ktimer_begin(s);
   int rc = dev_err(appnp::launch_split_copy(h, ld_h, n, f, fs, rw, main_of(0), rem_of(0),
                                             appnp::remainder_scale(g), s));
   ktimer_mark(s, APPNP_KT_COPY);
@@ -228,6 +265,7 @@ int propagate_split(const appnp_graph* g, const StepArgs& a0, const void* H, int
     am.out = last ? Z : main_of(dst);
     am.ld_out = last ? ld_z : fs;
     if (fs > 0) {
+      ktimer_begin(s);
       rc = dev_err(appnp::launch_step(APPNP_F32, appnp::EPI_FWD, 4, am, s));
       ktimer_mark(s, APPNP_KT_STEP);
     }
@@ -236,6 +274,7 @@ int propagate_split(const appnp_graph* g, const StepArgs& a0, const void* H, int
     // LPE = 1: nv = 4 into the next remainder buffer (the shipped form); LPE > 1: nv is always
     // the valid remainder columns, to_rem says where the row goes
     const int nv = (lpe == 1 && !last) ? 4 : (int)(f - fs);
+    ktimer_begin(s);
     rc = dev_err(appnp::launch_remainder(g, ar, appnp::EPI_FWD, rem_of(cur), h + fs, ld_h,
                                          last ? z + fs : rem_of(dst), last ? ld_z : rw, nv,
                                          !last, s));
@@ -257,6 +296,7 @@ int propagate_bwd_split(const appnp_graph* g, const StepArgs& a0, const void* dZ
   char* bufs[2] = {ws, ws + buf_b};
   auto main_of = [&](int i) { return reinterpret_cast<float*>(bufs[i]); };
   auto rem_of = [&](int i) { return reinterpret_cast<float*>(bufs[i] + main_b); };
+  ktimer_begin(s);
   int rc = dev_err(appnp::launch_split_copy(static_cast<const float*>(dZ), ld_dz, n, f, fs, rw,
                                             main_of(0), rem_of(0), appnp::remainder_scale(g),
                                             s));
@@ -278,12 +318,14 @@ int propagate_bwd_split(const appnp_graph* g, const StepArgs& a0, const void* dZ
     am.zin = main_of(cur);
     am.out = k == 0 ? nullptr : main_of(dst);
     if (fs > 0) {
+      ktimer_begin(s);
       rc = dev_err(appnp::launch_step(APPNP_F32, appnp::EPI_BWD, 4, am, s));
       ktimer_mark(s, APPNP_KT_STEP);
     }
     if (rc) break;
     set_drop(ar, p_drop, seed, k);
     ar.alpha = a_k;
+    ktimer_begin(s);
     rc = dev_err(appnp::launch_remainder(g, ar, appnp::EPI_BWD, rem_of(cur), dh_rem, ld_dh,
                                          k == 0 ? nullptr : rem_of(dst), rw, (int)(f - fs),
                                          true, s));
@@ -311,6 +353,9 @@ int appnp_abi_version(void) { return PPNP_AMD_ABI_VERSION; }
 
 const char* appnp_build_info(void) {
   return "src=" APPNP_SRC_DIGEST ";abi=" APPNP_STR(PPNP_AMD_ABI_VERSION) ";arch=" APPNP_ARCH
+#ifdef APPNP_TESTING
+      ";testing=1"
+#endif
       ";compiler=" __VERSION__ ";built=" __DATE__ " " __TIME__;
 }
 
@@ -337,8 +382,11 @@ int appnp_graph_create_rows(const int32_t* indptr, const int32_t* indices, const
   const int sb_lpe = (mode & APPNP_GRAPH_SB_W16) ? 4 : (mode & APPNP_GRAPH_SB_W8) ? 2 : 1;
   const bool want_sb = (mode & (APPNP_GRAPH_SOURCE_BLOCKS | APPNP_GRAPH_SB_W8 |
                                 APPNP_GRAPH_SB_W16)) != 0;
+  // the remainder columns the copy is sized for (0: its whole width 4 sb_lpe)
+  const int sb_cols = (mode & APPNP_GRAPH_SB_COLS_MASK) >> APPNP_GRAPH_SB_COLS_SHIFT;
+  if (sb_cols > 4 * sb_lpe) return APPNP_EINVAL;
   mode &= ~(APPNP_GRAPH_TRANSPOSE | APPNP_GRAPH_SOURCE_BLOCKS | APPNP_GRAPH_SB_W8 |
-            APPNP_GRAPH_SB_W16);
+            APPNP_GRAPH_SB_W16 | APPNP_GRAPH_SB_COLS_MASK);
   if (mode != APPNP_NORM_SYM && mode != APPNP_NORM_RW) return APPNP_EINVAL;
   if (row_lo < 0 || row_hi < row_lo || row_hi > n) return APPNP_EINVAL;
   if (want_t && (row_lo != 0 || row_hi != n)) return APPNP_EINVAL;
@@ -357,7 +405,8 @@ int appnp_graph_create_rows(const int32_t* indptr, const int32_t* indices, const
   // appnp_graph_source_blocks reports whether it was built.
   if (rc == APPNP_OK && want_sb) {
     const int sb =
-        appnp::graph_build_source_blocks(g, sb_lpe, indptr, indices, nnz, as_stream(stream));
+        appnp::graph_build_source_blocks(g, sb_lpe, sb_cols, indptr, indices, nnz,
+                                         as_stream(stream));
     if (sb != APPNP_OK && sb != APPNP_ENOTSUP && sb != APPNP_ERANGE && sb != APPNP_ENOMEM)
       rc = sb;
   }
@@ -464,6 +513,16 @@ int appnp_graph_source_block_layout(const appnp_graph* g, int* width, int64_t* e
   return APPNP_OK;
 }
 
+int appnp_graph_source_block_rows(const appnp_graph* g, int* cols, int* rows_per_group,
+                                  int64_t* direct_rows) {
+  if (!g) return APPNP_EINVAL;
+  const bool built = g->rb_off != nullptr;
+  if (cols) *cols = appnp::source_block_cols(g);
+  if (rows_per_group) *rows_per_group = built ? g->rb_rg : 0;
+  if (direct_rows) *direct_rows = built ? (g->row_hi - g->row_lo) - g->rb_direct_lo : 0;
+  return APPNP_OK;
+}
+
 int appnp_propagate_split_point(const appnp_graph* g, int64_t f, int dtype, int64_t* fs) {
   if (!g || !fs || f < 0 || !valid_dtype(dtype)) return APPNP_EINVAL;
   *fs = split_point(g, f, dtype, true);
@@ -487,8 +546,8 @@ int appnp_propagate(const appnp_graph* g, const void* H, int64_t ld_h, void* Z, 
   if (!H || !Z || ld_h < f || ld_z < f || H == Z) return APPNP_EINVAL;
   const hipStream_t s = as_stream(stream);
   const int64_t es = elem_size(dtype);
-  ktimer_start(s);
   if (K == 0) {
+    ktimer_begin(s);
     rc = dev_err(hipMemcpy2DAsync(Z, ld_z * es, H, ld_h * es, f * es, n,
                                   hipMemcpyDeviceToDevice, s));
     ktimer_mark(s, APPNP_KT_COPY);
@@ -537,6 +596,7 @@ int appnp_propagate(const appnp_graph* g, const void* H, int64_t ld_h, void* Z, 
     a.out = dst;
     a.ld_out = ld_dst;
     set_drop(a, p_drop, seed, k);
+    ktimer_begin(s);
     rc = dev_err(appnp::launch_step(dtype, appnp::EPI_FWD, V, a, s));
     ktimer_mark(s, APPNP_KT_STEP);
     if (rc) return rc;
@@ -561,8 +621,8 @@ int appnp_propagate_bwd(const appnp_graph* g, const void* dZ, int64_t ld_dz, voi
   if (!dZ || !dH || ld_dz < f || ld_dh < f || dZ == dH) return APPNP_EINVAL;
   const hipStream_t s = as_stream(stream);
   const int64_t es = elem_size(dtype);
-  ktimer_start(s);
   if (K == 0) {
+    ktimer_begin(s);
     rc = dev_err(hipMemcpy2DAsync(dH, ld_dh * es, dZ, ld_dz * es, f * es, n,
                                   hipMemcpyDeviceToDevice, s));
     ktimer_mark(s, APPNP_KT_COPY);
@@ -587,6 +647,7 @@ int appnp_propagate_bwd(const appnp_graph* g, const void* dZ, int64_t ld_dz, voi
 
   // dH = alpha * dZ  (the k = K term), then G_k = (1-alpha) M_k^T G_{k+1},
   // dH += alpha G_k (k >= 1) / dH += G_0.
+  ktimer_begin(s);
   rc = dev_err(appnp::launch_scale_rows(dtype, dZ, ld_dz, dH, ld_dh, n, f, alpha, s));
   ktimer_mark(s, APPNP_KT_COPY);
   if (rc) return rc;
@@ -631,6 +692,7 @@ int appnp_propagate_bwd(const appnp_graph* g, const void* dZ, int64_t ld_dz, voi
     a.ld_out = ld_w;
     a.alpha = k >= 1 ? alpha : 1.0f;
     set_drop(a, p_drop, seed, k);
+    ktimer_begin(s);
     rc = dev_err(appnp::launch_step(dtype, appnp::EPI_BWD, V, a, s));
     ktimer_mark(s, APPNP_KT_STEP);
     if (rc) return rc;
@@ -726,9 +788,9 @@ int appnp_step(const appnp_graph* g, int part, const void* Zin, int64_t ld_in, c
     }
   }
   const int V = appnp::pick_vec(dtype, f, lds, n_ld, ptrs, 4);
-  ktimer_start(as_stream(stream));
+  ktimer_begin(as_stream(stream));
   rc = dev_err(appnp::launch_step(dtype, epi, V, a, as_stream(stream)));
-  ktimer_mark(as_stream(stream), APPNP_KT_STEP);
+  ktimer_mark(as_stream(stream), part_kind(part));
   return rc;
 }
 
@@ -762,7 +824,7 @@ int appnp_split_copy(const appnp_graph* g, const float* H, int64_t ld_h, int64_t
   const void* ptrs[3] = {H, main, rem};
   if (!H || !rem || (fs > 0 && !main) || ld_h < f || !vec16(lds, 1, ptrs, 3)) return APPNP_EINVAL;
   const float* sc = appnp::remainder_scale(g);
-  ktimer_start(as_stream(stream));
+  ktimer_begin(as_stream(stream));
   const int rc = dev_err(appnp::launch_split_copy(H, ld_h, rows, f, fs, rw,
                                                   main ? main + g->row_lo * fs : nullptr,
                                                   rem + g->row_lo * rw,
@@ -798,7 +860,6 @@ int appnp_step_split(const appnp_graph* g, int part, const float* zin_main, cons
   const void* ptrs[8] = {zin_main, zin_rem, H, zout_main, zout_rem, Z, partial, nullptr};
   if (!vec16(lds, 3, ptrs, 7)) return APPNP_EINVAL;
   const hipStream_t s = as_stream(stream);
-  ktimer_start(s);
   StepArgs a = base_args(g, f, alpha);
   set_drop(a, p_drop, seed, k);
   if (fs > 0) {
@@ -837,8 +898,9 @@ int appnp_step_split(const appnp_graph* g, int part, const float* zin_main, cons
         am.ld_aux = ld_partial;
       }
     }
+    ktimer_begin(s);
     rc = dev_err(appnp::launch_step(APPNP_F32, epi, 4, am, s));
-    ktimer_mark(s, APPNP_KT_STEP);
+    ktimer_mark(s, part_kind(part));
     if (rc) return rc;
   }
   if (part == APPNP_PART_LOCAL) return APPNP_OK;  // the pass needs every row of zin_rem
@@ -846,6 +908,7 @@ int appnp_step_split(const appnp_graph* g, int part, const float* zin_main, cons
   // rows (a unit graph stores dr o y there), or into Z's last r columns
   const int nv = (g->rb_lpe == 1 && !to_z) ? 4 : (int)r;
   g->rem_launches.fetch_add(1, std::memory_order_relaxed);
+  ktimer_begin(s);
   rc = dev_err(appnp::launch_remainder(g, a, appnp::EPI_FWD, zin_rem, H + fs, ld_h,
                                        to_z ? Z + fs : zout_rem + g->row_lo * rw,
                                        to_z ? ld_z : rw, nv, !to_z, s));
@@ -859,9 +922,8 @@ int appnp_kernel_timer_begin(int max_launches, void* stream) {
   appnp::KTimer& t = appnp::g_ktimer;
   if (max_launches < 1 || max_launches > (1 << 20)) return APPNP_EINVAL;
   t.release();
-  t.ev.assign((size_t)max_launches + 1, nullptr);
-  t.st.assign(t.ev.size(), nullptr);
-  t.kind.assign(t.ev.size(), 0);
+  t.ev.assign(2 * (size_t)max_launches, nullptr);
+  t.kind.assign((size_t)max_launches, 0);
   for (hipEvent_t& e : t.ev) {
     if (hipEventCreate(&e) != hipSuccess) {
       e = nullptr;
@@ -870,8 +932,7 @@ int appnp_kernel_timer_begin(int max_launches, void* stream) {
     }
   }
   t.on = true;
-  (void)stream;  // the start event is recorded by the first timed entry point, right before its
-                 // first launch (ktimer_start), so no host time before the call is counted
+  (void)stream;  // every launch is bracketed by events on its own stream (ktimer_begin / _mark)
   return APPNP_OK;
 }
 
@@ -880,20 +941,49 @@ int appnp_kernel_timer_end(float* ms, int* kinds, int max, int* n_out) {
   if (!t.on) return APPNP_EINVAL;
   t.on = false;
   int rc = APPNP_OK;
-  for (int i = 0; i < t.n && rc == APPNP_OK; ++i) rc = dev_err(hipEventSynchronize(t.ev[i]));
-  const int launches = t.n > 0 ? t.n - 1 : 0;
-  for (int i = 1; i < t.n && i - 1 < max && rc == APPNP_OK; ++i) {
-    int j = i - 1;  // the previous event on the same stream
-    while (j >= 0 && t.st[j] != t.st[i]) --j;
+  for (int i = 0; i < 2 * t.n && rc == APPNP_OK; ++i)
+    rc = dev_err(hipEventSynchronize(t.ev[i]));
+  for (int i = 0; i < t.n && i < max && rc == APPNP_OK; ++i) {
     float e = NAN;
-    if (j >= 0 && hipEventElapsedTime(&e, t.ev[j], t.ev[i]) != hipSuccess) e = NAN;
-    if (ms) ms[i - 1] = e;
-    if (kinds) kinds[i - 1] = t.kind[i];
+    if (hipEventElapsedTime(&e, t.ev[2 * i], t.ev[2 * i + 1]) != hipSuccess) e = NAN;
+    if (ms) ms[i] = e;
+    if (kinds) kinds[i] = t.kind[i];
   }
-  if (n_out) *n_out = launches;
+  if (n_out) *n_out = t.n;
   if (rc == APPNP_OK && t.dropped) rc = APPNP_ERANGE;
   t.release();
   return rc;
+}
+
+// ---- tuning overrides (include/ppnp_amd.h) ------------------------------------------------
+
+const char* appnp_tuning_overrides(void) {
+  static const std::string s = [] {
+    std::string out;
+    if (!appnp::tuning_on()) return out;
+    for (const char* name : appnp::kTuningNames) {
+      const char* v = getenv(name);
+      if (!v || !*v) continue;
+      if (!out.empty()) out += ';';
+      out += name;
+      out += '=';
+      out += v;
+    }
+    return out;
+  }();
+  return s.c_str();
+}
+
+const char* appnp_tuning_names(void) {
+  static const std::string s = [] {
+    std::string out;
+    for (const char* name : appnp::kTuningNames) {
+      if (!out.empty()) out += ';';
+      out += name;
+    }
+    return out;
+  }();
+  return s.c_str();
 }
 
 // ---- captured plans: the K launches of appnp_propagate replayed as one hipGraph -----------

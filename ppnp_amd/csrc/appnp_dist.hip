@@ -122,10 +122,12 @@ int agree_split(appnp_dist* d, void* ws, hipStream_t s) {
   if (rc == APPNP_OK && d->split_ok)
     rc = dev_err(hipMemsetAsync(flags + kSlot * d->rank, 1, 1, s));
   if (rc == APPNP_OK) rc = d->allgather(flags, kSlot, d->rank, d->nranks, s, d->ctx);
-  // APPNP_DIST_TEST_AGREE_FAIL (tests): a failure on this rank after the exchange, so the
-  // poisoned handle can be observed
+#ifdef APPNP_TESTING
+  // APPNP_DIST_TEST_AGREE_FAIL (test library): a failure on this rank after the exchange, so
+  // the poisoned handle can be observed
   const char* inj = std::getenv("APPNP_DIST_TEST_AGREE_FAIL");
   if (rc == APPNP_OK && inj && *inj && std::atoi(inj)) rc = APPNP_EDEVICE;
+#endif
   for (int p = 0; p < d->nranks && rc == APPNP_OK; ++p)
     rc = dev_err(hipMemcpyAsync(&host[p], flags + kSlot * p, 1, hipMemcpyDeviceToHost, s));
   if (rc == APPNP_OK) rc = dev_err(hipStreamSynchronize(s));
@@ -133,6 +135,15 @@ int agree_split(appnp_dist* d, void* ws, hipStream_t s) {
     if (rc != APPNP_OK || host[p] != 1) d->split_ok = 0;
   if (rc != APPNP_OK) d->poisoned = rc;
   d->split_agreed = 1;
+  return rc;
+}
+
+// One exchange through the caller's all-gather on stream s, bracketed for the per-launch timer
+// (APPNP_KT_XCHG), so the time it takes is never counted in the launch that waits for it
+int exchange_on(appnp_dist* d, void* buf, size_t shard_bytes, hipStream_t s) {
+  appnp::ktimer_begin(s);
+  const int rc = d->allgather(buf, shard_bytes, d->rank, d->nranks, s, d->ctx);
+  appnp::ktimer_mark(s, APPNP_KT_XCHG);
   return rc;
 }
 
@@ -153,8 +164,8 @@ int propagate_split_rows(appnp_dist* d, const WsLayout& w, const float* H, int64
   const size_t rem_shard = (size_t)d->shard * (size_t)w.rw * 4;
   auto exchange = [&](int b, hipStream_t xs) {
     int rc = APPNP_OK;
-    if (w.fs > 0) rc = d->allgather(mainb[b], main_shard, d->rank, d->nranks, xs, d->ctx);
-    if (rc == APPNP_OK) rc = d->allgather(remb[b], rem_shard, d->rank, d->nranks, xs, d->ctx);
+    if (w.fs > 0) rc = exchange_on(d, mainb[b], main_shard, xs);
+    if (rc == APPNP_OK) rc = exchange_on(d, remb[b], rem_shard, xs);
     return rc;
   };
   int rc = appnp_split_copy(d->g, H, ld_h, f, w.fs ? mainb[0] : nullptr, remb[0], s);
@@ -345,7 +356,7 @@ int appnp_dist_propagate(appnp_dist* d, const void* H, int64_t ld_h, void* Z, in
   // Z_0: the held rows of H, then the whole of it by exchange (synchronous in stream order)
   int rc = dev_err(copy_rows(own(buf[0]), w.ld, H, ld_h, rows, f, es, s));
   if (rc == APPNP_OK && d->nranks > 1)
-    rc = d->allgather(buf[0], shard_bytes, d->rank, d->nranks, s, d->ctx);
+    rc = exchange_on(d, buf[0], shard_bytes, s);
   bool pending = false;  // an exchange on xs not yet waited for by `s`
   for (int k = 0; k < K && rc == APPNP_OK; ++k) {
     const bool last = k == K - 1;
@@ -371,11 +382,11 @@ int appnp_dist_propagate(appnp_dist* d, const void* H, int64_t ld_h, void* Z, in
     if (d->overlap) {
       rc = dev_err(hipEventRecord(d->produced, s));
       if (rc == APPNP_OK) rc = dev_err(hipStreamWaitEvent(d->xs, d->produced, 0));
-      if (rc == APPNP_OK) rc = d->allgather(next, shard_bytes, d->rank, d->nranks, d->xs, d->ctx);
+      if (rc == APPNP_OK) rc = exchange_on(d, next, shard_bytes, d->xs);
       if (rc == APPNP_OK) rc = dev_err(hipEventRecord(d->exchanged, d->xs));
       pending = rc == APPNP_OK;
     } else {
-      rc = d->allgather(next, shard_bytes, d->rank, d->nranks, s, d->ctx);
+      rc = exchange_on(d, next, shard_bytes, s);
     }
   }
   if (pending) (void)hipStreamWaitEvent(s, d->exchanged, 0);  // never leave xs running ahead

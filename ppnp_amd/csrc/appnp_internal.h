@@ -59,6 +59,9 @@ struct appnp_graph {
   int32_t rb_rg = 0;            // rows per group
   int32_t rb_passes = 0;
   int32_t rb_lpe = 0;           // lanes per entry of the pass: remainder rows of 4 rb_lpe columns
+  int32_t rb_pf = 0, rb_pc = 0; // LDS sums of a row: rb_pf 16-B pieces + rb_pc floats, i.e. the
+                                // pass is sized for 4 rb_pf + rb_pc remainder columns
+  int64_t rb_direct_lo = 0;     // held rows [rb_direct_lo, rows) are gathered directly (no group)
   double near_frac = 0.0;       // off-diagonal entries within kNearRows of their row / nnz
   // remainder-pass launches enqueued on this graph (appnp_graph_source_block_layout): the path
   // witness the tests read
@@ -90,8 +93,13 @@ hipError_t exclusive_scan(const int32_t* cnt, int64_t rows, int32_t* out, int64_
 // lpe: lanes per entry of the remainder pass (1, 2, 4: remainder rows of 4, 8, 16 columns)
 // a_indptr / a_indices / a_nnz: the whole graph's A (the row partition's gather-locality
 // measure is taken over all of it, so every rank decides the same split)
-int graph_build_source_blocks(appnp_graph* g, int lpe, const int32_t* a_indptr,
+// cols: remainder columns the pass is sized for (0: 4 lpe)
+int graph_build_source_blocks(appnp_graph* g, int lpe, int cols, const int32_t* a_indptr,
                               const int32_t* a_indices, int64_t a_nnz, hipStream_t s);
+// columns of the remainder the built copy holds sums for (0: no copy)
+inline int source_block_cols(const appnp_graph* g) {
+  return g->rb_off ? 4 * g->rb_pf + g->rb_pc : 0;
+}
 // to_rem: out is the next remainder buffer (a unit graph stores dr o y there), not Z / dH
 hipError_t launch_remainder(const appnp_graph* g, const StepArgs& a, int epi,
                             const float* z_rem, const float* h_rem, int64_t ld_h, float* out,
@@ -113,10 +121,17 @@ hipError_t launch_step(int dtype, int epi, int V, const StepArgs& a, hipStream_t
 hipError_t launch_scale_rows(int dtype, const void* src, int64_t ld_src, void* dst,
                              int64_t ld_dst, int64_t n, int64_t f, float alpha, hipStream_t s);
 
+// appnp_capi.hip: a tuning override (measurement only, tools/): `name` is read from the
+// environment when APPNP_TUNING=1, else dflt.  Each is read once, at its first use; every name
+// must be listed in kTuningNames (appnp_capi.hip), which appnp_tuning_overrides reports.
+int tuning_env(const char* name, int dflt);
+
 // appnp_capi.hip: the per-launch timer of appnp_kernel_timer_begin / _end.  While it is on
-// (on this thread), every launch of the propagation entry points is followed by a timing event
-// on its stream, tagged with the launch's kind (APPNP_KT_*).  Off: one thread-local load.
-void ktimer_start(hipStream_t s);  // the start event, right before a timed call's first launch
+// (on this thread), every launch (or exchange) of the propagation entry points is bracketed by
+// two timing events on its stream: ktimer_begin right before it, ktimer_mark right after it,
+// tagged with its kind (APPNP_KT_*).  So an interval covers that launch only, never a wait that
+// precedes it on the stream.  Off: one thread-local load each.
+void ktimer_begin(hipStream_t s);
 void ktimer_mark(hipStream_t s, int kind);
 
 // Leading dimension of the internal ping-pong buffers.  A random row gather costs 128-B line

@@ -22,14 +22,9 @@
 #include <algorithm>
 #include <cstdlib>
 
-#include "appnp_device.h"
+#include "appnp_internal.h"
 
 namespace appnp {
-
-static int env_int(const char* name, int dflt) {
-  const char* s = getenv(name);
-  return (s && *s) ? atoi(s) : dflt;
-}
 
 namespace {
 
@@ -459,14 +454,14 @@ hipError_t launch_step(int dtype, int epi, int V, const StepArgs& a_in, hipStrea
   // latency regime with hub rows (a wavefront per row): the widest vector, so a row needs the
   // fewest lanes and the most sub-groups walk the longest row at once (Cora-ML 5.94 -> 5.21 us
   // per iteration with V = 4 instead of 1; Citeseer 4.06 -> 3.89 us with V = 2)
-  static const int v_env = env_int("APPNP_VEC", -1);  // measurement override (<= pick_vec's)
+  static const int v_env = tuning_env("APPNP_VEC", -1);  // tuning override (<= pick_vec's)
   if (v_env > 0 && v_env <= v_max) V = v_env;
   const int G = lanes_for(V);
   // Bandwidth regime: a wavefront per row also for narrow F once rows are long on average
   // (products-synth slabs of 4-25 features, 51.5 entries a row: 6-10 % faster than G-lane
   // rows; uniform and power-law; arxiv-synth, 14.8 a row: G-lane rows 20-50 % faster).
   const bool long_rows = a.nnz >= (int64_t)kWideAvgRow * a.n_rows;
-  static const int wide_env = env_int("APPNP_WIDE", -1);  // measurement override
+  static const int wide_env = tuning_env("APPNP_WIDE", -1);  // tuning override
   const bool wide = wide_env >= 0 ? wide_env != 0
                                   : (G >= 16 || (latency && heavy_rows) || (!latency && long_rows));
   const int64_t slabs = (a.f + (int64_t)G * V - 1) / ((int64_t)G * V);
@@ -474,7 +469,7 @@ hipError_t launch_step(int dtype, int epi, int V, const StepArgs& a_in, hipStrea
   // one wave per row (wide) by default: measured best on products-synth (tools/tune.sh)
   // gridDim.x * 256 must stay below 2^32: cap at 4M blocks (grid-stride loops take the rest;
   // products-synth needs 612k, i.e. one wave per row)
-  static const int max_blocks = std::min(env_int("APPNP_MAX_BLOCKS", 1 << 22), 1 << 22);
+  static const int max_blocks = std::min(tuning_env("APPNP_MAX_BLOCKS", 1 << 22), 1 << 22);
   if (!wide || !a.hub) {
     a.hub = nullptr;
     a.n_hub = 0;
@@ -497,15 +492,15 @@ hipError_t launch_step(int dtype, int epi, int V, const StepArgs& a_in, hipStrea
   // (arxiv-synth, 14.8 a row): 1, 3 % faster than 2.  Small graphs with hub rows (latency
   // regime, wave per row because of them): 8, so the longest row -- which sets the launch
   // time -- takes few dependent rounds (Cora-ML 9.4 -> 5.8 us, Citeseer 5.4 -> 3.9 us).
-  static const int uw_env = env_int("APPNP_UW", -1);  // measurement override (1, 2, 4, 8)
+  static const int uw_env = tuning_env("APPNP_UW", -1);  // tuning override (1, 2, 4, 8)
   const int uw = uw_env > 0 ? uw_env : (latency && heavy_rows) ? 8 : (!latency && long_rows) ? 2 : 1;
   // cache policy of the streams (StepArgs::nt); APPNP_NT overrides for measurement
   // entries in flight per row of the narrow kernels: 8 in the latency regime, where a row's
   // dependent rounds set the launch time (pubmed-synth 5.77 -> 5.24 us, cora-sized uniform
   // 6.01 -> 5.45 us per iteration; tools/sweep_uw.sh), else 4
-  static const int un_env = env_int("APPNP_UN", -1);  // measurement override (4, 8)
+  static const int un_env = tuning_env("APPNP_UN", -1);  // tuning override (4, 8)
   const int un = un_env > 0 ? un_env : latency ? 8 : 4;
-  static const int nt_env = env_int("APPNP_NT", -1);
+  static const int nt_env = tuning_env("APPNP_NT", -1);
   a.nt = nt_env >= 0 ? nt_env : (latency ? 0 : 1);
   if (dtype == 0) {
     switch (epi) {

@@ -703,7 +703,7 @@ class NativeRowAPPNP:
         split layout (appnp_step_split)."""
         import ctypes as C
 
-        from .graph import remainder_width
+        from .graph import source_block_flags
 
         lib = _lib.load()
         self.device = torch.device(device)
@@ -730,8 +730,7 @@ class NativeRowAPPNP:
         val = None if data is None else data.to(self.device, torch.float32).contiguous()
         h = C.c_void_p()
         stream = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
-        w = remainder_width(n, int(features), dtype) if features else 0
-        sb = {0: 0, 4: _lib.GRAPH_SOURCE_BLOCKS, 8: _lib.GRAPH_SB_W8, 16: _lib.GRAPH_SB_W16}[w]
+        sb = source_block_flags(n, int(features), dtype) if features else 0
         _lib.check("appnp_dist_create", lib.appnp_dist_create(
             C.c_void_p(ip.data_ptr()), C.c_void_p(ix.data_ptr()) if ix.numel() else None,
             C.c_void_p(val.data_ptr()) if val is not None and val.numel() else None, n,

@@ -42,6 +42,19 @@ def remainder_width(n: int, features: int, dtype=torch.float32) -> int:
     return next((w for w in (4, 8, 16) if 1 <= r <= w), 0)
 
 
+def source_block_flags(n: int, features: int, dtype=torch.float32) -> int:
+    """The ``mode`` bits of the source-blocked copy for this shape (0: rows gathered whole):
+    APPNP_GRAPH_SOURCE_BLOCKS / _SB_W8 / _SB_W16 by ``remainder_width``, and for a W8 / W16 copy
+    APPNP_GRAPH_SB_COLS(r), r the remainder columns, so the pass keeps 4 r bytes of sums per row
+    and holds more rows per row pass (13-column slabs: 3 passes instead of 4 on products-synth)."""
+    w = remainder_width(n, features, dtype)
+    if not w:
+        return 0
+    r = features % 32 if features > 32 else features
+    flag = {4: _lib.GRAPH_SOURCE_BLOCKS, 8: _lib.GRAPH_SB_W8, 16: _lib.GRAPH_SB_W16}[w]
+    return flag | (_lib.GRAPH_SB_COLS(r) if w > 4 else 0)
+
+
 def splits_rows(n: int, features: int, dtype=torch.float32) -> bool:
     """Whether appnp_propagate takes the split path for this shape on a graph built with the
     matching source-blocked copy (``remainder_width`` > 0)."""
@@ -58,8 +71,13 @@ def source_block_layout_of(handle):
                    C.byref(launches)))
     if w.value == 0:
         return None
+    cols, rg, direct = C.c_int(), C.c_int(), C.c_int64()
+    _lib.check("appnp_graph_source_block_rows",
+               _lib.load().appnp_graph_source_block_rows(handle, C.byref(cols), C.byref(rg),
+                                                         C.byref(direct)))
     return {"width": w.value, "entries": ent.value, "value_free": bool(vf.value),
-            "row_passes": rp.value, "launches": launches.value}
+            "row_passes": rp.value, "launches": launches.value, "cols": cols.value,
+            "rows_per_group": rg.value, "direct_rows": direct.value}
 
 
 def split_layout_of(handle, f: int):
@@ -141,14 +159,13 @@ class Graph:
             raise ValueError("indptr must have n+1 entries")
         nnz = int(ix.numel())
         row_hi = n if row_hi is None else int(row_hi)
-        width = 4
+        sb_flag = _lib.GRAPH_SOURCE_BLOCKS
         if features is not None:
-            width = remainder_width(n, int(features), dtype) or 4
+            sb_flag = source_block_flags(n, int(features), dtype) or _lib.GRAPH_SOURCE_BLOCKS
         if source_blocks is None:
             # full graphs (appnp_propagate) and the held rows of a row partition
             # (appnp_step_split) alike
             source_blocks = features is not None and splits_rows(n, int(features), dtype)
-        sb_flag = {4: _lib.GRAPH_SOURCE_BLOCKS, 8: _lib.GRAPH_SB_W8, 16: _lib.GRAPH_SB_W16}[width]
         flags = ((_lib.GRAPH_TRANSPOSE if transpose else 0)
                  | (sb_flag if source_blocks else 0))
         lib = _lib.load()

@@ -226,14 +226,17 @@ class PropagatePlan:
             pass
 
 
-KERNEL_KINDS = {_lib.KT_COPY: "copy", _lib.KT_STEP: "step", _lib.KT_REM: "rem"}
+KERNEL_KINDS = {_lib.KT_COPY: "copy", _lib.KT_STEP: "step", _lib.KT_REM: "rem",
+                _lib.KT_LOCAL: "local", _lib.KT_REMOTE: "remote", _lib.KT_XCHG: "xchg"}
 
 
 def kernel_times(fn, device, max_launches: int = 1024) -> list[tuple[str, float]]:
     """Call ``fn()`` with the library's per-launch timer on (``appnp_kernel_timer_begin`` /
     ``_end``) and return one (kind, ms) pair per launch it enqueued, in launch order: "copy"
-    (the split copy), "step" (the SpMM kernel), "rem" (the remainder pass).  The events sit on
-    the launch stream between launches that are stream-ordered anyway; no profiler runs."""
+    (the split copy), "step" (the SpMM kernel), "local" / "remote" (its two halves on a
+    row-partitioned graph), "rem" (the remainder pass), "xchg" (an exchange of the library's
+    own row loop).  Each interval is bracketed by events right before and after its launch on
+    the launch stream, so no wait before it is counted; no profiler runs."""
     lib = _lib.load()
     with torch.cuda.device(device):
         # fn() runs even if the timer cannot start: at N > 1 it may hold collectives that every

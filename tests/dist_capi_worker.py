@@ -71,6 +71,11 @@ def main():
     indptr, indices = synth.graph_for(a.workload, device=dev)
     H = synth.features(n, F, dtype=dtype, device=dev, seed=1)
 
+    if rank == a.sb_oom_rank or a.agree_fail:
+        # fault injection needs libppnp_amd_test.so (the product library has no hooks): the
+        # test sets PPNP_AMD_LIB; fail loudly rather than run without the injected fault
+        if "testing=1" not in _lib.load().appnp_build_info().decode():
+            raise SystemExit("fault injection needs PPNP_AMD_LIB=" + _lib.TEST_LIB_PATH)
     if rank == a.sb_oom_rank:
         os.environ["APPNP_SB_TEST_OOM"] = "1"
     runner = pdist.NativeRowAPPNP(indptr, indices, n, dev, overlap=a.overlap,

@@ -23,6 +23,15 @@ import torch.distributed as dist
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+def _require_test_library():
+    """Fault injection needs libppnp_amd_test.so (the product library has no hooks): the test
+    sets PPNP_AMD_LIB; fail loudly rather than run without the injected fault."""
+    from ppnp_amd import _lib
+
+    if "testing=1" not in _lib.load().appnp_build_info().decode():
+        raise SystemExit("fault injection needs PPNP_AMD_LIB=" + _lib.TEST_LIB_PATH)
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--layout", default="col")
@@ -81,6 +90,7 @@ def main():
         indptr, indices = synth.uniform_graph(a.n, a.m, 7, device=dev)
     H = synth.features(a.n, a.f, device=dev, seed=1)
     if rank == a.sb_oom_rank:
+        _require_test_library()
         os.environ["APPNP_SB_TEST_OOM"] = "1"
     runner = pdist.PartitionedAPPNP.create(indptr, indices, a.n, H, a.K, a.alpha, dev,
                                            layout=layout, overlap=a.overlap,

@@ -41,7 +41,7 @@ def test_abi_version_and_strerror():
     from ppnp_amd import _lib
 
     lib = _lib.load()
-    assert lib.appnp_abi_version() == 1
+    assert lib.appnp_abi_version() == _lib.ABI_VERSION == 2
     assert lib.appnp_strerror(0) == b"ok"
     assert lib.appnp_strerror(_lib.APPNP_EINVAL) == b"invalid argument"
     assert lib.appnp_strerror(_lib.APPNP_ENOTSUP) == b"not supported"
@@ -153,3 +153,45 @@ def test_torch_library_ops_registered_with_fake_kernels():
         from ppnp_amd.graph import Graph
 
         Graph.lookup(10**9)  # not a live graph: loud, no fallback
+
+
+def test_product_library_carries_no_test_or_measurement_hooks():
+    """the fault injectors of the tests live in libppnp_amd_test.so only
+    (-DAPPNP_TESTING), and the losing XCD-pacing experiment is gone, so the shipped library
+    names none of them; the test library does name its hooks."""
+    from ppnp_amd import _lib
+
+    prod = open(_lib.LIB_PATH, "rb").read()
+    for bad in (b"_TEST_", b"_PACE_", b"APPNP_SB_MAX_BLOCKS", b"ALLHIT"):
+        assert bad not in prod, bad
+    test = open(_lib.TEST_LIB_PATH, "rb").read()
+    for hook in (b"APPNP_SB_TEST_OOM", b"APPNP_SB_MAX_BLOCKS", b"APPNP_DIST_TEST_AGREE_FAIL"):
+        assert hook in test, hook
+
+
+def _overrides_in_child(env_extra):
+    import subprocess
+    import sys
+
+    env = {k: v for k, v in os.environ.items() if not k.startswith("APPNP_")}
+    env.update(env_extra, PYTHONPATH=ROOT)
+    code = ("from ppnp_amd import _lib; lib = _lib.load(); "
+            "print(lib.appnp_tuning_overrides().decode() + '|' + "
+            "lib.appnp_tuning_names().decode())")
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                         timeout=120, check=True).stdout.strip().splitlines()[-1]
+    active, names = out.split("|")
+    return active, names.split(";")
+
+
+def test_tuning_overrides_need_APPNP_TUNING():
+    """a stray tuning variable in the environment changes nothing unless
+    APPNP_TUNING=1 is set too, and then appnp_tuning_overrides names it (bench.py prints it as
+    build.overrides)."""
+    active, names = _overrides_in_child({"APPNP_UW": "4", "APPNP_SPLIT": "0"})
+    assert active == ""
+    assert {"APPNP_UW", "APPNP_SPLIT", "APPNP_VEC", "APPNP_REM_SYNC_W16"} <= set(names)
+    active, _ = _overrides_in_child({"APPNP_UW": "4", "APPNP_SPLIT": "0", "APPNP_TUNING": "1"})
+    assert active == "APPNP_SPLIT=0;APPNP_UW=4"
+    active, _ = _overrides_in_child({"APPNP_TUNING": "1"})
+    assert active == ""

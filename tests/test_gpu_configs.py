@@ -174,6 +174,25 @@ def test_products_k10_bf16_matches_oracle(products):
     assert float((Z.argmax(1) == ref.argmax(1)).double().mean()) >= 0.98
 
 
+def test_products_col8_slab_three_row_passes(products):
+    """the 13-column slab of F = 100 on 8 column ranks (rank 0 of the
+    exchange-free 8-GPU layout) on its own W16 copy sized for 13 columns: 3 row passes of 196
+    rows per wave group and 40,581 rows gathered directly (round 5: 4 passes), every value of
+    Z_K, K = 10, against the float64 torch.sparse loop of the same A_hat."""
+    import ppnp_amd
+
+    _, H, K, alpha, a, adj = products
+    G = ppnp_amd.Graph.from_scipy(adj, device=DEV, features=13)
+    sb = G.source_block_layout()
+    assert (sb["width"], sb["cols"], sb["row_passes"], sb["rows_per_group"],
+            sb["direct_rows"]) == (16, 13, 3, 196, 40_581), sb
+    assert G.remainder_cols(13) == 13
+    H13 = H[:, :13].contiguous()
+    Z = ppnp_amd.propagate_forward(G, H13, K, alpha).cpu()
+    _check_full(Z, O.appnp_propagate_torch_cpu(a, H13.cpu().double(), K, alpha))
+    G.close()
+
+
 def test_products_powerlaw_k10_matches_oracle():
     """The Chung-Lu power-law graph with products' node and edge counts (hub rows: the heavy /
     hub lists of the main SpMM and long runs in the remainder pass) at full size, K = 10."""
@@ -450,8 +469,12 @@ def test_split_decision_is_collective():
     """The regrouped copy is best-effort: when it cannot be built on ONE rank (rank 1 here,
     APPNP_SB_TEST_OOM), every rank keeps whole rows -- both the Python row loop (an all-reduce at
     create) and the library's engine (one small exchange at the first propagation) -- instead
-    of exchanging two parts on some ranks and one on others.  Results still match."""
-    env = dict(os.environ, PPNP_DIST_BACKEND="gloo", PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
+    of exchanging two parts on some ranks and one on others.  Results still match.  The fault
+    is injected through the test library (libppnp_amd_test.so): the product one has no hooks."""
+    from ppnp_amd import _lib
+
+    env = dict(os.environ, PPNP_DIST_BACKEND="gloo", PYTHONPATH=ROOT, OMP_NUM_THREADS="2",
+               PPNP_AMD_LIB=_lib.TEST_LIB_PATH)
     base = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
             "--master-addr=127.0.0.1"]
     py = base + [f"--master-port={_free_port()}", os.path.join(ROOT, "tests", "dist_worker.py"),
@@ -489,8 +512,11 @@ def test_native_row_engine_poisoned_after_failed_agreement():
     """a split agreement that fails after its exchange poisons the handle.  Both
     ranks inject the failure (APPNP_DIST_TEST_AGREE_FAIL), so neither waits on the other: the
     first call returns APPNP_EDEVICE after the agreement's one exchange, and the second returns
-    the stored code without exchanging again."""
-    env = dict(os.environ, PPNP_DIST_BACKEND="gloo", PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
+    the stored code without exchanging again.  (Test library: the product one has no hooks.)"""
+    from ppnp_amd import _lib
+
+    env = dict(os.environ, PPNP_DIST_BACKEND="gloo", PYTHONPATH=ROOT, OMP_NUM_THREADS="2",
+               PPNP_AMD_LIB=_lib.TEST_LIB_PATH)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
            os.path.join(ROOT, "tests", "dist_capi_worker.py"), "--workload", "arxiv-synth",

@@ -271,27 +271,39 @@ def test_source_blocks_only_when_requested():
     assert ppnp_amd.Graph.from_scipy(a, device=DEV, features=7).source_block_bytes() > 0  # W8
 
 
-def test_source_blocks_best_effort_fallback(monkeypatch, ahat):
-    """ADVICE r1: a graph whose regrouped copy cannot be built (here: more source blocks than
-    the limit, lowered for the test) is still created, warns, and gathers whole rows --
-    with the same results."""
-    import ppnp_amd
+def _hook_child(case, ahat, H, K, tmp_path):
+    """Run tests/hook_worker.py on the test library (libppnp_amd_test.so, the product library
+    has no fault hooks) and return its Z."""
+    import os
+    import subprocess
+    import sys
 
-    monkeypatch.setenv("APPNP_SB_MAX_BLOCKS", "2")  # N = 300k needs 10 blocks of 2^15
-    with pytest.warns(RuntimeWarning, match="could not be built"):
-        G = ppnp_amd.Graph.from_csr(ahat.indptr, ahat.indices, None, N, device=DEV,
-                                    source_blocks=True)
-    assert G.source_block_bytes() == 0 and G.split_point(100) == 0
+    from ppnp_amd import _lib
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    data, out = tmp_path / "in.npz", tmp_path / "out.npz"
+    np.savez(data, indptr=ahat.indptr.astype(np.int32), indices=ahat.indices.astype(np.int32),
+             n=np.int64(N), H=H.numpy())
+    env = dict(os.environ, PPNP_AMD_LIB=_lib.TEST_LIB_PATH, PYTHONPATH=root)
+    proc = subprocess.run([sys.executable, os.path.join(root, "tests", "hook_worker.py"),
+                           "--case", case, "--data", str(data), "--out", str(out),
+                           "--K", str(K)],
+                          env=env, cwd=root, capture_output=True, text=True, timeout=110)
+    assert proc.returncode == 0, proc.stdout[-3000:] + proc.stderr[-3000:]
+    return np.load(out)["Z"]
+
+
+def test_source_blocks_best_effort_fallback(ahat, tmp_path):
+    """ADVICE r1: a graph whose regrouped copy cannot be built (here: more source blocks than
+    the limit, lowered for the test through the test library's APPNP_SB_MAX_BLOCKS) is still
+    created, warns, and gathers whole rows -- with the same results."""
     H = _h(100, 31)
-    Z = ppnp_amd.propagate_forward(G, H.to(DEV), 2, 0.1)
+    Z = _hook_child("max-blocks", ahat, H, 2, tmp_path)
     # ahat's pattern is A + I; an unweighted graph of that pattern (self loops merged) has the
     # same A_hat up to the diagonal weight 2 -- compare against the oracle of that graph
-    import scipy.sparse as sp
-
     a = sp.csr_matrix((np.ones(ahat.nnz, dtype=np.float32), ahat.indices, ahat.indptr),
                       shape=ahat.shape)
-    close_fp32(Z.double().cpu().numpy(), O.appnp_propagate(O.calc_a_hat(a, "sym"), H.numpy(), 2,
-                                                           0.1))
+    close_fp32(Z, O.appnp_propagate(O.calc_a_hat(a, "sym"), H.numpy(), 2, 0.1))
 
 
 # ---- wider remainders: APPNP_GRAPH_SB_W8 / APPNP_GRAPH_SB_W16 (2 / 4 lanes per entry) --------
@@ -300,11 +312,13 @@ def test_source_blocks_best_effort_fallback(monkeypatch, ahat):
 @pytest.fixture(scope="module")
 def wide(adj):
     """Graphs whose source-blocked copy is laid out for 8 and 16 remainder columns (chosen by
-    Graph from the named width: 40 = 32 + 8, narrow rows of 13)."""
+    Graph from the named width: 40 = 32 + 8, narrow rows of 16; a copy is sized for the
+    remainder it is named for, APPNP_GRAPH_SB_COLS, so 13 would serve at most 13 columns)."""
     import ppnp_amd
 
     g8 = ppnp_amd.Graph.from_scipy(adj, device=DEV, features=40)
-    g16 = ppnp_amd.Graph.from_scipy(adj, device=DEV, features=13)
+    g16 = ppnp_amd.Graph.from_scipy(adj, device=DEV, features=16)
+    assert g16.source_block_layout()["cols"] == 16 and g8.source_block_layout()["cols"] == 8
     assert g8.source_block_bytes() > 0 and g16.source_block_bytes() > 0
     return {8: g8, 16: g16}
 
@@ -429,24 +443,16 @@ def test_narrow_rows_on_the_four_column_layout(graphs, ahat, f):
         close_fp32(dH.double().cpu().numpy(), O.appnp_backward(ahat, H.numpy(), 3, 0.1))
 
 
-def test_source_blocks_enomem_leaves_no_stale_error(monkeypatch, ahat):
-    """a regrouped copy whose allocation really fails (APPNP_SB_TEST_OOM asks for
-    2^60 bytes) is tolerated -- the graph is created without it, warns, and the failed
-    hipMalloc's error is cleared, so the first propagation and an unrelated torch kernel both
-    succeed."""
-    import ppnp_amd
-
-    monkeypatch.setenv("APPNP_SB_TEST_OOM", "1")
-    with pytest.warns(RuntimeWarning, match="could not be built"):
-        G = ppnp_amd.Graph.from_csr(ahat.indptr, ahat.indices, None, N, device=DEV,
-                                    source_blocks=True)
-    monkeypatch.delenv("APPNP_SB_TEST_OOM")
-    assert G.source_block_layout() is None and G.remainder_cols(100) == 0
-    H = _h(100, 37).to(DEV)
-    Z = ppnp_amd.propagate_forward(G, H, 3, 0.1)
-    x = torch.arange(1 << 20, device=DEV, dtype=torch.float32).sum()
-    torch.cuda.synchronize()
-    assert torch.isfinite(Z).all() and float(x) > 0
+def test_source_blocks_enomem_leaves_no_stale_error(ahat, tmp_path):
+    """a regrouped copy whose allocation really fails (the test library's
+    APPNP_SB_TEST_OOM asks for 2^60 bytes) is tolerated -- the graph is created without it,
+    warns, and the failed hipMalloc's error is cleared, so the first propagation and an
+    unrelated torch kernel both succeed (checked in the child), with the oracle's result."""
+    H = _h(100, 37)
+    Z = _hook_child("oom", ahat, H, 3, tmp_path)
+    a = sp.csr_matrix((np.ones(ahat.nnz, dtype=np.float32), ahat.indices, ahat.indptr),
+                      shape=ahat.shape)
+    close_fp32(Z, O.appnp_propagate(O.calc_a_hat(a, "sym"), H.numpy(), 3, 0.1))
 
 
 def test_workspace_covers_the_wide_split_layout(wide):
@@ -499,3 +505,53 @@ def test_split_from_line_aligned_h(graphs, ahat, f, ld, p):
     dH = ppnp_amd.propagate_backward(G, Hb[:, :f], 3, 0.1, p_drop=p, seed=5)
     close_fp32(dH.double().cpu().numpy(),
                O.appnp_backward(ahat, H.numpy(), 3, 0.1, p_drop=p, seed=5))
+
+
+# ---- packed sums and direct rows (APPNP_GRAPH_SB_COLS) -------------------
+
+
+def _direct_n(f):
+    """Nodes for which a W16 pass sized for f columns needs 1 row pass plus direct rows: one
+    pass holds 256 CUs x 16 waves x (160 KiB / (16 x 4 f)) rows (802,816 at f = 13); 1/16 more
+    rows than that are gathered directly (<= 1/8: the second pass is dropped)."""
+    cap = 256 * 16 * (163840 // (16 * 4 * f))
+    return cap + cap // 16
+
+
+@pytest.mark.parametrize("f,p,weighted", [(13, 0.0, False), (13, 0.3, True), (11, 0.3, False),
+                                          (9, 0.0, True)])
+def test_direct_rows_match_oracle(f, p, weighted):
+    """A W16 copy sized for f columns keeps 4 f bytes of sums per row (f = 13: 3 pieces + 1
+    float; 11: 2 + 3; 9: 2 + 1), so the rows past one row pass are gathered straight from the
+    CSR: forward (with edge dropout) and the adjoint on the value-free (unit) layout and on a
+    weighted graph (values), against the float64 oracle; the layout reports 1 pass + the rest
+    direct, and the copy serves only remainders of at most f columns."""
+    import ppnp_amd
+    from ppnp_amd import _lib
+    from ppnp_amd.graph import source_block_flags
+
+    n = _direct_n(f)
+    a = O.synth_graph(n, 2 * n, seed=20 + f)
+    if weighted:
+        a.data = (1.0 + (np.arange(a.nnz) % 7) / 4.0).astype(np.float32)
+        a = ((a + a.T) * 0.5).tocsr()
+    a.sort_indices()
+    ahat = O.calc_a_hat(a, "sym")
+    # Graph.from_csr(features=f) asks for the copy sized for f columns
+    assert source_block_flags(n, f) == _lib.GRAPH_SB_W16 | _lib.GRAPH_SB_COLS(f)
+    G = ppnp_amd.Graph.from_scipy(a, device=DEV, features=f)
+    sb = G.source_block_layout()
+    cap = 256 * 16 * (163840 // (16 * 4 * f))
+    assert sb["cols"] == f and sb["row_passes"] == 1 and sb["value_free"] == (not weighted)
+    assert sb["direct_rows"] == n - cap > 0, sb
+    assert G.remainder_cols(f) == f and G.remainder_cols(f + 1) == 0  # sized for f only
+    H = torch.from_numpy(np.random.default_rng(f).standard_normal((n, f)).astype(np.float32))
+    Z = ppnp_amd.propagate_forward(G, H.to(DEV), 3, 0.1, p_drop=p, seed=9)
+    close_fp32(Z.double().cpu().numpy(), O.appnp_propagate(ahat, H.numpy(), 3, 0.1, p_drop=p,
+                                                            seed=9))
+    dH = ppnp_amd.propagate_backward(G, H.to(DEV), 3, 0.1, p_drop=p, seed=9)
+    close_fp32(dH.double().cpu().numpy(), O.appnp_backward(ahat, H.numpy(), 3, 0.1, p_drop=p,
+                                                           seed=9))
+    # bitwise deterministic: the direct rows sum in a fixed order (a butterfly per piece)
+    assert torch.equal(Z, ppnp_amd.propagate_forward(G, H.to(DEV), 3, 0.1, p_drop=p, seed=9))
+    G.close()
