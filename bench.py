@@ -116,6 +116,10 @@ def parse(argv=None):
     p.add_argument("--exchange", default="multipath", choices=["multipath", "group", "native"],
                    help="R x C layouts: relayed exchange over every rank, or one all-gather "
                         "per column group; row layouts: 'native' runs the library's own loop")
+    p.add_argument("--pipeline", default="auto", choices=["auto", "on", "off"],
+                   help="row layouts with overlap and >= 3 row groups: exchange by one broadcast "
+                        "per row shard and run the product per group of arrived shards (auto: "
+                        "whenever it applies)")
     p.add_argument("--candidate-timeout", type=float, default=240.0,
                    help="N > 1: seconds one layout candidate (build, warm-up, timed steps, "
                         "parity) may take before the run is ended with the best line so far")
@@ -223,14 +227,15 @@ def device_info(dev) -> dict:
     return out
 
 
-def traffic_key(workload, dtype_name, kernel_key, f_local, rows, overlap=False) -> str:
+def traffic_key(workload, dtype_name, kernel_key, f_local, rows, overlap=False,
+                pipeline=False) -> str:
     """Key of the PMC traffic of one rank's iteration: what the rank RUNS -- the workload, the
     dtype, the iteration's kernels, its feature slab width and held rows, the local/remote split
     of overlap mode -- and a digest of the kernel sources.  Not the layout's name: rank r of a
     real P-rank run and ``--emulate P:r`` on one GPU run the same kernels on the same share, so a
     profile of the emulation is the traffic of the real rank (VERDICT r3 missing #3), and a
     profile of other kernels, another share or an older build of them never matches."""
-    ov = ":ov" if overlap else ""
+    ov = (":ov" if overlap else "") + (":pipe" if pipeline else "")
     return (f"{workload}:{dtype_name}:{kernel_key}:F{f_local}:rows{rows}{ov}"
             f":src={src_digest()}")
 
@@ -335,7 +340,8 @@ def rank_traffic_key(workload, dtype_name, runner, K) -> str:
     ``--emulate P:r`` (tests/test_bench_roofline.py pins it)."""
     kkey = rank_kernel_plan(runner, K)[1]
     return traffic_key(workload, dtype_name, kkey, runner.width, runner.graph.rows,
-                       bool(getattr(runner, "overlap", False)))
+                       bool(getattr(runner, "overlap", False)),
+                       bool(getattr(runner, "pipeline", False)))
 
 
 def rem_row_layout(rows, lpe, cols=None):
@@ -979,6 +985,8 @@ def main(argv=None):
         ref_max = float(Zref.abs().max()) if Zref is not None else 0.0
         ref_name = "single-GPU appnp_propagate of the whole graph, per rank (max over ranks)"
 
+    pipeline = {"auto": None, "on": True, "off": False}[args.pipeline]
+
     def measure(cand):
         layout, overlap, exchange = cand
         if world > 1 and layout.rows > 1:
@@ -986,15 +994,17 @@ def main(argv=None):
         t1 = time.perf_counter()
         runner = pdist.PartitionedAPPNP.create(indptr, indices, n, H, K, alpha, dev,
                                                layout=layout, overlap=overlap,
-                                               exchange=exchange, **emu)
+                                               exchange=exchange, pipeline=pipeline, **emu)
         torch.cuda.synchronize()
         t_build = time.perf_counter() - t1
         try:
             box = box_line_rate()
             wall, dev_ms, steps_ms = time_steps(runner.run, stream, args.steps, args.warmup,
                                                 world, ctl)
-            par = (cand_name(cand) if not args.emulate else
-                   cand_name(cand) + f"-EMULATED-rank{args.emulate}")
+            par = cand_name(cand) + ("-pipelined" if getattr(runner, "pipeline", False)
+                                     else "")
+            if args.emulate:
+                par += f"-EMULATED-rank{args.emulate}"
             R = runner.layout.rows
             # the other row shards of this rank's column group land here every iteration
             exchange_in = ((R - 1) * runner.shard * runner.width * esz

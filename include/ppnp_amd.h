@@ -310,6 +310,47 @@ int appnp_step_split(const appnp_graph* g, int part, const float* zin_main, cons
                      float alpha, float p_drop, uint64_t seed, void* stream);
 
 /*
+ * Pipelined row steps.  A row rank's product split by
+ * SOURCE SHARD: with the held rows' entries grouped by the shard of their column (rank s of P
+ * holds rows [s S, (s+1) S)), the product over the shards that have already arrived can run while
+ * the others are still in flight, one launch per group of shards, so only the last group's share
+ * of the compute is left after the exchange ends.
+ *
+ * appnp_graph_shard_offsets  build the held rows' shard offsets (nshards = P, shard_rows = S,
+ *                            P S >= n; (P + 1) x rows int32 of device memory).  Allocates and
+ *                            synchronises; idempotent for the same P and S.
+ * appnp_step_shards          one iteration's product over the entries of the held rows whose
+ *                            column lies in shards [s_lo, s_hi) (fp32):
+ *                              APPNP_SHARDS_FIRST  partial  = (1-alpha) sum
+ *                              APPNP_SHARDS_ACC    partial += (1-alpha) sum
+ *                              APPNP_SHARDS_LAST   Zout     = (1-alpha) sum + partial + alpha H
+ *                              APPNP_SHARDS_ONLY   Zout     = (1-alpha) sum + alpha H
+ *                            Zin: all n rows (only the range's rows are read); partial [held rows,
+ *                            f] fp32.  Summing every shard once, in any grouping, gives the
+ *                            appnp_step result up to fp32 summation order.
+ * appnp_step_split_shards    the same on the split layout of appnp_step_split: the main columns
+ *                            take the shard range and mode; LAST / ONLY then run the remainder
+ *                            pass (which needs every row of zin_rem) and write zout_* or Z.
+ * Stream-ordered, no allocation; the dropout hash is the same as appnp_step's.
+ */
+enum appnp_shard_mode {
+  APPNP_SHARDS_FIRST = 0,
+  APPNP_SHARDS_ACC = 1,
+  APPNP_SHARDS_LAST = 2,
+  APPNP_SHARDS_ONLY = 3
+};
+int appnp_graph_shard_offsets(appnp_graph* g, int nshards, int64_t shard_rows, void* stream);
+int appnp_step_shards(const appnp_graph* g, int s_lo, int s_hi, int mode, const float* Zin,
+                      int64_t ld_in, const float* H, int64_t ld_h, float* Zout, int64_t ld_out,
+                      float* partial, int64_t ld_partial, int64_t f, int k, float alpha,
+                      float p_drop, uint64_t seed, void* stream);
+int appnp_step_split_shards(const appnp_graph* g, int s_lo, int s_hi, int mode,
+                            const float* zin_main, const float* zin_rem, const float* H,
+                            int64_t ld_h, float* zout_main, float* zout_rem, float* Z,
+                            int64_t ld_z, float* partial, int64_t ld_partial, int64_t f, int k,
+                            float alpha, float p_drop, uint64_t seed, void* stream);
+
+/*
  * A captured propagation plan: the K launches of appnp_propagate for FIXED buffers (H, Z, ws)
  * and parameters, recorded once into a hipGraph and replayed by appnp_plan_launch on any
  * stream with a single graph launch.  For small, launch-bound graphs and serving loops that
@@ -388,6 +429,28 @@ int appnp_dist_propagate(appnp_dist* d, const void* H, int64_t ld_h, void* Z, in
                          int64_t f, int dtype, int K, float alpha, float p_drop, uint64_t seed,
                          void* ws, size_t ws_bytes, void* stream);
 void appnp_dist_destroy(appnp_dist* d);
+
+/*
+ * The pipelined exchange of the row loop.  With overlap and
+ * P >= 3 ranks, a broadcast callback makes appnp_dist_propagate send every iterate as P in-place
+ * broadcasts, one row shard each (roots 0 .. P-1 in turn, on the engine's exchange stream, each
+ * followed by an event), and run the product as appnp_step(_split)_shards launches: FIRST on the
+ * rank's own shard, then ACC per group of arrived remote shards (sized 1, 2, 4, ... from the last
+ * to arrive, appnp_dist_pipeline_groups), LAST on the last group -- so after the exchange only
+ * one shard's share of the product is left instead of every remote shard's.  The split layout's
+ * remainder part keeps the all-gather (it is exchanged first).  Collective: every rank sets it.
+ * appnp_bcast_fn: in-place broadcast of `bytes` at `buf` from rank `root` to every rank, in stream
+ * order on `stream` (ncclBroadcast(buf, buf, bytes, ncclChar, root, comm, stream) for RCCL:
+ * appnp_bcast_rccl), or synchronous; returns 0 or a negative code.
+ * appnp_dist_set_broadcast builds the held rows' shard offsets (allocates, synchronises `stream`);
+ * APPNP_ENOTSUP without overlap or with P < 3 (one remote shard: nothing to pipeline).
+ */
+typedef int (*appnp_bcast_fn)(void* buf, size_t bytes, int root, int nranks, void* stream,
+                              void* ctx);
+int appnp_dist_set_broadcast(appnp_dist* d, appnp_bcast_fn fn, void* ctx, void* stream);
+/* The groups [lo[i], hi[i]) of remote shards, *n_out of them (0: not pipelined). */
+int appnp_dist_pipeline_groups(const appnp_dist* d, int* lo, int* hi, int max, int* n_out);
+int appnp_bcast_rccl(void* buf, size_t bytes, int root, int nranks, void* stream, void* ctx);
 
 /* appnp_allgather_fn over RCCL; ctx is the ncclComm_t of the P ranks, rank order = row order.
  * RCCL is resolved at first use (the librccl.so.1 already loaded in the process, e.g.

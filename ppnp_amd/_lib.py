@@ -41,6 +41,7 @@ def GRAPH_SB_COLS(c: int) -> int:
 
 F32, BF16 = 0, 1
 PART_ALL, PART_LOCAL, PART_REMOTE = 0, 1, 2
+SHARDS_FIRST, SHARDS_ACC, SHARDS_LAST, SHARDS_ONLY = 0, 1, 2, 3  # appnp_shard_mode
 KT_COPY, KT_STEP, KT_REM, KT_LOCAL, KT_REMOTE, KT_XCHG = 1, 2, 3, 4, 5, 6  # appnp_kernel_kind
 
 _vp, _i64, _i32, _f32, _u64, _sz = C.c_void_p, C.c_int64, C.c_int, C.c_float, C.c_uint64, C.c_size_t
@@ -108,6 +109,9 @@ _SIGS = {
     ),
     "appnp_dist_destroy": (None, [_vp]),
     "appnp_allgather_rccl": (_i32, [_vp, _sz, _i32, _i32, _vp, _vp]),
+    "appnp_bcast_rccl": (_i32, [_vp, _sz, _i32, _i32, _vp, _vp]),
+    "appnp_dist_set_broadcast": (_i32, [_vp, _vp, _vp, _vp]),
+    "appnp_dist_pipeline_groups": (_i32, [_vp, _vp, _vp, _i32, C.POINTER(_i32)]),
     "appnp_line_rate_probe": (_i32, [_vp, _i64, _i64, _u64, _vp, _vp]),
     "appnp_kernel_timer_begin": (_i32, [_i32, _vp]),
     "appnp_kernel_timer_end": (_i32, [_vp, _vp, _i32, C.POINTER(_i32)]),
@@ -119,6 +123,17 @@ _SIGS = {
         _i32,
         [_vp, _i32, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _f32,
          _f32, _u64, _vp],
+    ),
+    "appnp_graph_shard_offsets": (_i32, [_vp, _i32, _i64, _vp]),
+    "appnp_step_shards": (
+        _i32,
+        [_vp, _i32, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _i64, _i32, _f32,
+         _f32, _u64, _vp],
+    ),
+    "appnp_step_split_shards": (
+        _i32,
+        [_vp, _i32, _i32, _i32, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _i64, _vp, _i64, _i64, _i32,
+         _f32, _f32, _u64, _vp],
     ),
     "appnp_split_layout": (_i32, [_vp, _i64, C.POINTER(_i64), C.POINTER(_i64)]),
     "appnp_split_copy": (_i32, [_vp, _vp, _i64, _i64, _vp, _vp, _vp]),
@@ -133,6 +148,8 @@ EXPORTED = tuple(_SIGS)
 
 # appnp_allgather_fn (include/ppnp_amd.h): in-place all-gather of equal row shards
 ALLGATHER_FN = C.CFUNCTYPE(_i32, _vp, _sz, _i32, _i32, _vp, _vp)
+# appnp_bcast_fn: in-place broadcast of one row shard from its owner
+BCAST_FN = C.CFUNCTYPE(_i32, _vp, _sz, _i32, _i32, _vp, _vp)
 
 _lib = None
 

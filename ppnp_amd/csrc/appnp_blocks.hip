@@ -276,33 +276,47 @@ __device__ __forceinline__ void rem_finish_piece(const StepArgs& a, const RemLay
   }
 }
 
-// The wave's LDS sums of a row group: piece q of row `row` is accA[row * pf + q] for q < pf,
-// the first pc floats of piece pf are accB[row * pc ..]; the rest of a row is never stored (its
-// columns lie past the remainder the copy was sized for, and gather zeros).  LPE = 1: accA only.
+// The wave's LDS sums of a row group, piece-major: piece q of row `row` is accA[q * rg + row]
+// for q < pf, float c < pc of piece pf is accB[c * rg + row]; the rest of a row is never stored
+// (its columns lie past the remainder the copy was sized for, and gather zeros).  LPE = 1: accA
+// only.  Piece-major, the tails of one piece in a lane group (8 lanes of a 16-B access) hit
+// consecutive 16-B slots for consecutive rows; row-major (a 64-B row stride on a W16 copy) put
+// every row of one parity in the same 4 banks -- 4-way conflicts, 2.2e8 extra LDS cycles per
+// launch of the 13-column slab's pass (SQ_LDS_BANK_CONFLICT, profiles/r6_w16_sq.txt).
+#ifdef APPNP_REM_ROW_MAJOR  // measurement variant: the round-5 row-major sums
+#define REM_SLOT(q, row) ((row) * L.pf + (q))
+#else
+#define REM_SLOT(q, row) ((q) * L.rg + (row))
+#endif
 template <int LPE>
 __device__ __forceinline__ void acc_add(f32x4* accA, float* accB, const RemLayout& L, int row,
                                         int q, const f32x4& v) {
   if (LPE == 1 || q < L.pf) {
-    f32x4& s = accA[LPE == 1 ? row : row * L.pf + q];
+    f32x4& s = accA[LPE == 1 ? row : REM_SLOT(q, row)];
     s = f32x4{s.x + v.x, s.y + v.y, s.z + v.z, s.w + v.w};
   } else if (q == L.pf && L.pc > 0) {
-    float* b = accB + row * L.pc;
-    b[0] += v.x;
-    if (L.pc > 1) b[1] += v.y;
-    if (L.pc > 2) b[2] += v.z;
+    // LDS float adds without a return (ds_add_f32): no read to wait for on this short path.
+    // Not for atomicity -- a (row, piece) has one tail per chunk, and the wave that owns the
+    // row adds its chunks in order, so the sums stay deterministic
+    float* b = accB + row;
+    __hip_atomic_fetch_add(b, v.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    if (L.pc > 1)
+      __hip_atomic_fetch_add(b + L.rg, v.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    if (L.pc > 2)
+      __hip_atomic_fetch_add(b + 2 * L.rg, v.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
   }
 }
 
 template <int LPE>
 __device__ __forceinline__ f32x4 acc_get(const f32x4* accA, const float* accB, const RemLayout& L,
                                          int row, int q) {
-  if (LPE == 1 || q < L.pf) return accA[LPE == 1 ? row : row * L.pf + q];
+  if (LPE == 1 || q < L.pf) return accA[LPE == 1 ? row : REM_SLOT(q, row)];
   f32x4 v = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
   if (q == L.pf && L.pc > 0) {
-    const float* b = accB + row * L.pc;
+    const float* b = accB + row;
     v.x = b[0];
-    if (L.pc > 1) v.y = b[1];
-    if (L.pc > 2) v.z = b[2];
+    if (L.pc > 1) v.y = b[L.rg];
+    if (L.pc > 2) v.z = b[2 * L.rg];
   }
   return v;
 }
@@ -318,23 +332,34 @@ __device__ __forceinline__ void rem_walk(const StepArgs& a, const RemLayout& L,
   const int lane = threadIdx.x & (kWave - 1);
   const int q = lane / CH, le = lane % CH;
   const uint32_t cmask = (1u << kRemColBits) - 1u;
-  for (int32_t c = c_begin; c < c_end; c += U) {
-    const int nch = min(U, c_end - c);
-    int32_t cb[U];  // first source row of each chunk's block (wave-uniform: scalar loads)
-    uint32_t en[U];
-    float wt[U];
+  // the entries of chunks [c0, c0 + U): first source row of each chunk's block (wave-uniform:
+  // scalar loads), packed entry, value
+  auto fetch = [&](int32_t c0, int32_t (&cbx)[U], uint32_t (&enx)[U], float (&wtx)[U]) {
+    const int n = min(U, c_end - c0);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      cb[u] = 0;
-      en[u] = kRemNone;
-      wt[u] = 1.0f;
-      if (u < nch) {
-        const int64_t e = (int64_t)(c + u) * CH + le;
-        cb[u] = L.cblk[c + u] << L.br_log2;
-        en[u] = ld_nt<uint32_t>(L.ent + e);
-        if constexpr (!VF) wt[u] = ld_nt<float>(L.val + e);
+      cbx[u] = 0;
+      enx[u] = kRemNone;
+      wtx[u] = 1.0f;
+      if (u < n) {
+        const int64_t e = (int64_t)(c0 + u) * CH + le;
+        cbx[u] = L.cblk[c0 + u] << L.br_log2;
+        enx[u] = ld_nt<uint32_t>(L.ent + e);
+        if constexpr (!VF) wtx[u] = ld_nt<float>(L.val + e);
       }
     }
+  };
+  int32_t cb[U];
+  uint32_t en[U];
+  float wt[U];
+#ifdef APPNP_REM_PREFETCH
+  fetch(c_begin, cb, en, wt);
+#endif
+  for (int32_t c = c_begin; c < c_end; c += U) {
+    const int nch = min(U, c_end - c);
+#ifndef APPNP_REM_PREFETCH
+    fetch(c, cb, en, wt);
+#endif
     f32x4 zv[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -349,6 +374,13 @@ __device__ __forceinline__ void rem_walk(const StepArgs& a, const RemLayout& L,
                     : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
       }
     }
+#ifdef APPNP_REM_PREFETCH
+    // measurement variant: the next chunks' entries load under this iteration's gathers
+    int32_t cbn[U];
+    uint32_t enn[U];
+    float wtn[U];
+    fetch(c + U, cbn, enn, wtn);
+#endif
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       if (u >= nch) break;  // wave-uniform
@@ -370,6 +402,14 @@ __device__ __forceinline__ void rem_walk(const StepArgs& a, const RemLayout& L,
       const bool tail = le == CH - 1 || ((heads >> (lane + 1)) & 1ull);
       if (act && tail) acc_add<LPE>(accA, accB, L, row, q, v);
     }
+#ifdef APPNP_REM_PREFETCH
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      cb[u] = cbn[u];
+      en[u] = enn[u];
+      wt[u] = wtn[u];
+    }
+#endif
   }
 }
 
@@ -464,8 +504,8 @@ __global__ __launch_bounds__(kRemThreads) void k_rem_persist(StepArgs a, RemLayo
     const int64_t g = (int64_t)p * L.slots + slot;
     const int64_t r0 = g * L.rg;
     const int rows = (int)max<int64_t>(0, min<int64_t>(L.rg, held - r0));
-    for (int r = lane; r < rows * L.pf; r += kWave) accA[r] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    for (int r = lane; r < rows * L.pc; r += kWave) accB[r] = 0.0f;
+    for (int r = lane; r < L.rg * L.pf; r += kWave) accA[r] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    for (int r = lane; r < L.rg * L.pc; r += kWave) accB[r] = 0.0f;
     if (L.sync > 0) {
       // every wave runs the same nb blocks (an empty segment is 0 chunks) in the same steps,
       // so every wave reaches every barrier; a wave's segments are contiguous in its stream
@@ -482,6 +522,7 @@ __global__ __launch_bounds__(kRemThreads) void k_rem_persist(StepArgs a, RemLayo
     if constexpr (LPE == 1) {
       for (int r = lane; r < rows; r += kWave) rem_finish<EPI, VF>(a, L, r0 + r, accA[r]);
     } else {
+      // row-major over (row, piece), so a wave's stores cover whole rows of the output
       for (int r = lane; r < rows * LPE; r += kWave)
         rem_finish_piece<EPI, VF, LPE>(a, L, r0 + r / LPE, r % LPE,
                                        acc_get<LPE>(accA, accB, L, r / LPE, r % LPE));
@@ -691,6 +732,9 @@ int graph_build_source_blocks(appnp_graph* g, int lpe, int cols, const int32_t* 
   if (lpe != 1 && lpe != 2 && lpe != 4) return APPNP_EINVAL;
   if (lpe == 1 || cols <= 0) cols = 4 * lpe;
   if (cols > 4 * lpe) return APPNP_EINVAL;
+  // APPNP_SB_COLS (tuning override): size the pass for more columns than requested (A/B of the
+  // packed sums); never fewer, which would drop the requested ones
+  if (lpe > 1) cols = std::min(4 * lpe, std::max(cols, tuning_env("APPNP_SB_COLS", 0)));
   const int pf = cols / 4, pc = cols % 4;  // RemLayout::pf / pc
   const int chunk = kRemChunk / lpe;     // entries per chunk (one per lpe lanes)
   // rows per wave group: 16 waves x max_rg rows x 4 cols bytes of LDS
@@ -726,7 +770,10 @@ int graph_build_source_blocks(appnp_graph* g, int lpe, int cols, const int32_t* 
   // those rows straight from the CSR (one line request per nonzero) rather than refill the
   // whole table on every XCD once more
   int64_t direct_lo = rows;
-  if (passes > 1 && rows - (passes - 1) * cap <= rows / 8) {
+  // APPNP_SB_DIRECT (tuning override): the 1/d share of the rows below which they go direct
+  // (0: never)
+  static const int direct_den = tuning_env("APPNP_SB_DIRECT", 8);
+  if (passes > 1 && direct_den > 0 && rows - (passes - 1) * cap <= rows / direct_den) {
     passes -= 1;
     rg = max_rg;
     direct_lo = passes * cap;

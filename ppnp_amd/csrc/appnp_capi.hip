@@ -78,7 +78,8 @@ void ktimer_mark(hipStream_t s, int kind) {
 const char* const kTuningNames[] = {
     "APPNP_SPLIT",       "APPNP_VEC",         "APPNP_WIDE",         "APPNP_UW",
     "APPNP_UN",          "APPNP_NT",          "APPNP_MAX_BLOCKS",   "APPNP_REM_SYNC_W4",
-    "APPNP_REM_SYNC_W8", "APPNP_REM_SYNC_W16", "APPNP_SB_ROWS",     "APPNP_REM_VF"};
+    "APPNP_REM_SYNC_W8", "APPNP_REM_SYNC_W16", "APPNP_SB_ROWS",     "APPNP_REM_VF",
+    "APPNP_SB_COLS",     "APPNP_SB_DIRECT"};
 
 bool tuning_on() {
   static const bool on = [] {
@@ -906,6 +907,156 @@ int appnp_step_split(const appnp_graph* g, int part, const float* zin_main, cons
   if (part == APPNP_PART_LOCAL) return APPNP_OK;  // the pass needs every row of zin_rem
   // the remainder pass over every source block: into the next remainder buffer at the held
   // rows (a unit graph stores dr o y there), or into Z's last r columns
+  const int nv = (g->rb_lpe == 1 && !to_z) ? 4 : (int)r;
+  g->rem_launches.fetch_add(1, std::memory_order_relaxed);
+  ktimer_begin(s);
+  rc = dev_err(appnp::launch_remainder(g, a, appnp::EPI_FWD, zin_rem, H + fs, ld_h,
+                                       to_z ? Z + fs : zout_rem + g->row_lo * rw,
+                                       to_z ? ld_z : rw, nv, !to_z, s));
+  ktimer_mark(s, APPNP_KT_REM);
+  return rc;
+}
+
+// ---- pipelined row steps: the held rows' entries of a range of source shards -------------
+
+int appnp_graph_shard_offsets(appnp_graph* g, int nshards, int64_t shard_rows, void* stream) {
+  if (!g) return APPNP_EINVAL;
+  return appnp::graph_build_shard_offsets(g, nshards, shard_rows, as_stream(stream));
+}
+
+namespace {
+
+// The step's CSR restricted to the held rows' entries with a column in shards [s_lo, s_hi), and
+// the epilogue of `mode` (appnp_shard_mode): FIRST partial = y, ACC partial += y, LAST out = y +
+// partial + alpha H, ONLY out = y + alpha H.  Returns APPNP_OK or a code.
+int shard_step_args(const appnp_graph* g, int s_lo, int s_hi, int mode, StepArgs& a, int* epi) {
+  if (!g->sh_off) return APPNP_EINVAL;  // appnp_graph_shard_offsets first
+  if (s_lo < 0 || s_hi > g->sh_n || s_lo >= s_hi) return APPNP_EINVAL;
+  const int64_t rows = g->row_hi - g->row_lo;
+  a.row_ptr = g->sh_off + (int64_t)s_lo * rows;
+  a.row_end = g->sh_off + (int64_t)s_hi * rows;
+  // the kernel shape follows the average row length: the range's share of the entries
+  a.nnz = g->nnz_hat * (int64_t)(s_hi - s_lo) / g->sh_n;
+  a.heavy = nullptr;  // the heavy / hub lists describe whole rows, not their shard ranges
+  a.n_heavy = 0;
+  a.hub = nullptr;
+  a.n_hub = 0;
+  switch (mode) {
+    case APPNP_SHARDS_FIRST: *epi = appnp::EPI_PARTIAL; return APPNP_OK;
+    case APPNP_SHARDS_ACC: *epi = appnp::EPI_ACCUM; return APPNP_OK;
+    case APPNP_SHARDS_LAST: *epi = appnp::EPI_FINISH; return APPNP_OK;
+    case APPNP_SHARDS_ONLY: *epi = appnp::EPI_FWD; return APPNP_OK;
+    default: return APPNP_EINVAL;
+  }
+}
+
+inline int shard_kind(int mode) {
+  return mode == APPNP_SHARDS_FIRST ? APPNP_KT_LOCAL : APPNP_KT_REMOTE;
+}
+
+}  // namespace
+
+int appnp_step_shards(const appnp_graph* g, int s_lo, int s_hi, int mode, const float* Zin,
+                      int64_t ld_in, const float* H, int64_t ld_h, float* Zout, int64_t ld_out,
+                      float* partial, int64_t ld_partial, int64_t f, int k, float alpha,
+                      float p_drop, uint64_t seed, void* stream) {
+  int rc = check_common(g, f, APPNP_F32, 0, alpha, p_drop);
+  if (rc) return rc;
+  if (k < 0) return APPNP_EINVAL;
+  const int64_t rows = g->row_hi - g->row_lo;
+  StepArgs a = base_args(g, f, alpha);
+  int epi = appnp::EPI_FWD;
+  rc = shard_step_args(g, s_lo, s_hi, mode, a, &epi);
+  if (rc) return rc;
+  if (rows == 0 || f == 0) return APPNP_OK;
+  const bool to_partial = mode == APPNP_SHARDS_FIRST || mode == APPNP_SHARDS_ACC;
+  const bool reads_partial = mode == APPNP_SHARDS_ACC || mode == APPNP_SHARDS_LAST;
+  const bool reads_h = mode == APPNP_SHARDS_LAST || mode == APPNP_SHARDS_ONLY;
+  if (!Zin || ld_in < f) return APPNP_EINVAL;
+  if ((to_partial || reads_partial) && (!partial || ld_partial < f)) return APPNP_EINVAL;
+  if (!to_partial && (!Zout || ld_out < f)) return APPNP_EINVAL;
+  if (reads_h && (!H || ld_h < f)) return APPNP_EINVAL;
+  a.zin = Zin;
+  a.ld_in = ld_in;
+  a.out = to_partial ? static_cast<void*>(partial) : static_cast<void*>(Zout);
+  a.ld_out = to_partial ? ld_partial : ld_out;
+  if (reads_h) {
+    a.h = H;
+    a.ld_h = ld_h;
+  }
+  if (mode == APPNP_SHARDS_LAST) {
+    a.aux = partial;
+    a.ld_aux = ld_partial;
+  }
+  set_drop(a, p_drop, seed, k);
+  const int64_t lds[4] = {ld_in, a.ld_out, reads_h ? ld_h : ld_in,
+                          reads_partial ? ld_partial : ld_in};
+  const void* ptrs[4] = {Zin, a.out, reads_h ? H : nullptr, reads_partial ? partial : nullptr};
+  const int V = appnp::pick_vec(APPNP_F32, f, lds, 4, ptrs, 4);
+  const hipStream_t s = as_stream(stream);
+  ktimer_begin(s);
+  rc = dev_err(appnp::launch_step(APPNP_F32, epi, V, a, s));
+  ktimer_mark(s, shard_kind(mode));
+  return rc;
+}
+
+int appnp_step_split_shards(const appnp_graph* g, int s_lo, int s_hi, int mode,
+                            const float* zin_main, const float* zin_rem, const float* H,
+                            int64_t ld_h, float* zout_main, float* zout_rem, float* Z,
+                            int64_t ld_z, float* partial, int64_t ld_partial, int64_t f, int k,
+                            float alpha, float p_drop, uint64_t seed, void* stream) {
+  int rc = check_common(g, f, APPNP_F32, 0, alpha, p_drop);
+  if (rc) return rc;
+  if (k < 0) return APPNP_EINVAL;
+  const int64_t r = rows_split(g, f);
+  if (!r) return APPNP_ENOTSUP;
+  const int64_t rows = g->row_hi - g->row_lo, fs = f - r, rw = 4 * (int64_t)g->rb_lpe;
+  StepArgs a = base_args(g, f, alpha);
+  StepArgs am = a;
+  int epi = appnp::EPI_FWD;
+  rc = shard_step_args(g, s_lo, s_hi, mode, am, &epi);
+  if (rc) return rc;
+  if (rows == 0 || f == 0) return APPNP_OK;
+  const bool to_partial = mode == APPNP_SHARDS_FIRST || mode == APPNP_SHARDS_ACC;
+  const bool reads_partial = mode == APPNP_SHARDS_ACC || mode == APPNP_SHARDS_LAST;
+  const bool finishes = !to_partial;  // LAST / ONLY: the row's output, then the remainder pass
+  const bool to_z = Z != nullptr;
+  if (fs == 0 && mode != APPNP_SHARDS_ONLY) return APPNP_EINVAL;  // nothing to pipeline
+  if (fs > 0 && !zin_main) return APPNP_EINVAL;
+  if (finishes && (!zin_rem || !H || ld_h < f)) return APPNP_EINVAL;
+  if (finishes && !to_z && (!zout_rem || (fs > 0 && !zout_main))) return APPNP_EINVAL;
+  if (to_z && ld_z < f) return APPNP_EINVAL;
+  if ((to_partial || reads_partial) && (!partial || ld_partial < fs)) return APPNP_EINVAL;
+  const int64_t lds[3] = {finishes ? ld_h : 4, to_z ? ld_z : 4,
+                          (to_partial || reads_partial) ? ld_partial : 4};
+  const void* ptrs[8] = {zin_main, zin_rem, H, zout_main, zout_rem, Z, partial, nullptr};
+  if (!vec16(lds, 3, ptrs, 7)) return APPNP_EINVAL;
+  const hipStream_t s = as_stream(stream);
+  set_drop(a, p_drop, seed, k);
+  set_drop(am, p_drop, seed, k);
+  if (fs > 0) {
+    am.f = (int32_t)fs;
+    am.zin = zin_main;
+    am.ld_in = fs;
+    if (to_partial) {
+      am.out = partial;
+      am.ld_out = ld_partial;
+    } else {
+      am.out = to_z ? static_cast<void*>(Z) : static_cast<void*>(zout_main + g->row_lo * fs);
+      am.ld_out = to_z ? ld_z : fs;
+      am.h = H;
+      am.ld_h = ld_h;
+      if (reads_partial) {
+        am.aux = partial;
+        am.ld_aux = ld_partial;
+      }
+    }
+    ktimer_begin(s);
+    rc = dev_err(appnp::launch_step(APPNP_F32, epi, 4, am, s));
+    ktimer_mark(s, shard_kind(mode));
+    if (rc) return rc;
+  }
+  if (!finishes) return APPNP_OK;  // the pass needs every row of zin_rem
   const int nv = (g->rb_lpe == 1 && !to_z) ? 4 : (int)r;
   g->rem_launches.fetch_add(1, std::memory_order_relaxed);
   ktimer_begin(s);

@@ -15,12 +15,17 @@ constexpr int kWavesPerBlock = kBlock / kWave;
 // Epilogue of one propagation step (y = scale * sum_j w_ij Zin[j]):
 //   FWD      out = y + alpha * H                    (forward iteration)
 //   BWD      out = y (if out != null); aux += alpha * y   (adjoint iteration; aux = dH)
-//   PARTIAL  out(fp32) = y                          (local-column half of a split step)
-//   FINISH   out = y + aux(fp32) + alpha * H        (remote-column half of a split step)
-enum Epi { EPI_FWD = 0, EPI_BWD = 1, EPI_PARTIAL = 2, EPI_FINISH = 3 };
+//   PARTIAL  out(fp32) = y                          (local-column half of a split step; the
+//                                                    first shard group of a pipelined one)
+//   FINISH   out = y + aux(fp32) + alpha * H        (remote-column half of a split step; the
+//                                                    last shard group of a pipelined one)
+//   ACCUM    out(fp32) += y                         (a middle shard group of a pipelined step)
+enum Epi { EPI_FWD = 0, EPI_BWD = 1, EPI_PARTIAL = 2, EPI_FINISH = 3, EPI_ACCUM = 4 };
 
 struct StepArgs {
   const int32_t* row_ptr;  // local rows, row_ptr[0] == 0
+  const int32_t* row_end;  // null: row i's entries end at row_ptr[i + 1]; else at row_end[i]
+                           // (a shard range of the held rows: appnp_step_shards)
   const int32_t* col;      // global column index
   const float* val;        // A_hat values (fp32)
   const void* zin;         // all n rows (global index)
@@ -52,6 +57,11 @@ struct StepArgs {
   float* rem_dh;           // remainder pass, adjoint: dH's remainder columns (rows x ld_rem_dh)
   int64_t ld_rem_dh;
 };
+
+// End of row i's entries in the step's CSR (StepArgs::row_end)
+__device__ __forceinline__ int32_t row_end_of(const StepArgs& a, int64_t i) {
+  return a.row_end ? a.row_end[i] : a.row_ptr[i + 1];
+}
 
 constexpr int kHeavyRow = 32;   // a row longer than this gets a whole wavefront (narrow)
 constexpr int kHubRow = 512;    // ... and one longer than this is dispatched first (wide)

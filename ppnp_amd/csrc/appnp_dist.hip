@@ -48,6 +48,12 @@ struct appnp_dist {
   hipStream_t xs = nullptr;            // exchange stream (overlap)
   hipEvent_t produced = nullptr;       // dst rows written on the caller's stream
   hipEvent_t exchanged = nullptr;      // exchange finished on xs
+  // pipelined exchange (appnp_dist_set_broadcast): one broadcast per row shard on xs, each
+  // followed by its event, and the groups of remote shards the product waits for in turn
+  appnp_bcast_fn bcast = nullptr;
+  void* bctx = nullptr;
+  std::vector<hipEvent_t> arrived;     // [nranks]: shard r has landed (on xs)
+  std::vector<std::pair<int, int>> groups;
 };
 
 namespace {
@@ -147,6 +153,50 @@ int exchange_on(appnp_dist* d, void* buf, size_t shard_bytes, hipStream_t s) {
   return rc;
 }
 
+// The pipelined exchange of one iterate: xs waits for the producer, then broadcasts row shard r
+// from rank r, r = 0 .. P-1 in turn (the same order on every rank), each bracketed for the timer
+// and followed by its arrival event.
+int exchange_shards(appnp_dist* d, char* full, size_t shard_bytes, hipStream_t s) {
+  int rc = dev_err(hipEventRecord(d->produced, s));
+  if (rc == APPNP_OK) rc = dev_err(hipStreamWaitEvent(d->xs, d->produced, 0));
+  for (int r = 0; r < d->nranks && rc == APPNP_OK; ++r) {
+    appnp::ktimer_begin(d->xs);
+    rc = d->bcast(full + (size_t)r * shard_bytes, shard_bytes, r, d->nranks, d->xs, d->bctx);
+    appnp::ktimer_mark(d->xs, APPNP_KT_XCHG);
+    if (rc == APPNP_OK) rc = dev_err(hipEventRecord(d->arrived[r], d->xs));
+  }
+  return rc;
+}
+
+// Groups of remote shards in arrival order (ppnp_amd/dist.py shard_groups): sized 1, 2, 4, ...
+// from the last to arrive backwards, cut where a group would span the own shard.
+std::vector<std::pair<int, int>> shard_groups(int R, int ri) {
+  std::vector<int> arrival;
+  for (int s = 0; s < R; ++s)
+    if (s != ri) arrival.push_back(s);
+  std::vector<int> sizes;
+  for (int left = (int)arrival.size(), sz = 1; left > 0; sz *= 2) {
+    const int take = std::min(sz, left);
+    sizes.push_back(take);
+    left -= take;
+  }
+  std::vector<std::pair<int, int>> groups;
+  size_t pos = 0;
+  for (auto it = sizes.rbegin(); it != sizes.rend(); ++it) {
+    int start = arrival[pos];
+    for (int j = 0; j < *it; ++j) {
+      const int a = arrival[pos + j];
+      const bool end = j + 1 == *it || arrival[pos + j + 1] != a + 1;
+      if (end) {
+        groups.emplace_back(start, a + 1);
+        if (j + 1 < *it) start = arrival[pos + j + 1];
+      }
+    }
+    pos += *it;
+  }
+  return groups;
+}
+
 bool aligned16(const void* p, int64_t ld) {
   return ld % 4 == 0 && (reinterpret_cast<uintptr_t>(p) % 16) == 0;
 }
@@ -211,6 +261,100 @@ int propagate_split_rows(appnp_dist* d, const WsLayout& w, const float* H, int64
   return rc;
 }
 
+hipError_t copy_rows(void* dst, int64_t ld_dst, const void* src, int64_t ld_src, int64_t rows,
+                     int64_t f, int64_t es, hipStream_t s);
+
+// appnp_dist_propagate on the split layout with the pipelined exchange: the remainder part is
+// all-gathered first on xs, the main part by one broadcast per shard; the main product runs FIRST
+// on the own shard, ACC per group of arrived shards, LAST on the last group (then the remainder
+// pass, after the remainder part's exchange).
+int propagate_split_rows_pipelined(appnp_dist* d, const WsLayout& w, const float* H, int64_t ld_h,
+                                   float* Z, int64_t ld_z, int64_t f, int K, float alpha,
+                                   float p_drop, uint64_t seed, char* base, hipStream_t s) {
+  float* mainb[2] = {reinterpret_cast<float*>(base),
+                     reinterpret_cast<float*>(base + w.part_bytes)};
+  float* remb[2] = {reinterpret_cast<float*>(base + w.main_bytes),
+                    reinterpret_cast<float*>(base + w.part_bytes + w.main_bytes)};
+  float* partial = reinterpret_cast<float*>(base + 2 * w.part_bytes);
+  const size_t main_shard = (size_t)d->shard * (size_t)w.fs * 4;
+  const size_t rem_shard = (size_t)d->shard * (size_t)w.rw * 4;
+  auto exchange = [&](int b) {
+    // the remainder part first (small: it lands before the main shards), then the main part
+    int rc = dev_err(hipEventRecord(d->produced, s));
+    if (rc == APPNP_OK) rc = dev_err(hipStreamWaitEvent(d->xs, d->produced, 0));
+    if (rc == APPNP_OK) rc = exchange_on(d, remb[b], rem_shard, d->xs);
+    if (rc == APPNP_OK) rc = dev_err(hipEventRecord(d->exchanged, d->xs));
+    if (rc == APPNP_OK) rc = exchange_shards(d, reinterpret_cast<char*>(mainb[b]), main_shard, s);
+    return rc;
+  };
+  const int ri = d->rank;
+  int rc = appnp_split_copy(d->g, H, ld_h, f, mainb[0], remb[0], s);
+  if (rc == APPNP_OK) rc = exchange(0);
+  for (int k = 0; k < K && rc == APPNP_OK; ++k) {
+    const bool last = k == K - 1;
+    const int cur = k & 1, nxt = cur ^ 1;
+    rc = appnp_step_split_shards(d->g, ri, ri + 1, APPNP_SHARDS_FIRST, mainb[cur], nullptr,
+                                 nullptr, 0, nullptr, nullptr, nullptr, 0, partial, w.fs, f, k,
+                                 alpha, p_drop, seed, s);
+    for (size_t i = 0; i < d->groups.size() && rc == APPNP_OK; ++i) {
+      const int a = d->groups[i].first, b = d->groups[i].second;
+      rc = dev_err(hipStreamWaitEvent(s, d->arrived[b - 1], 0));
+      if (rc != APPNP_OK) break;
+      if (i + 1 < d->groups.size()) {
+        rc = appnp_step_split_shards(d->g, a, b, APPNP_SHARDS_ACC, mainb[cur], nullptr, nullptr,
+                                     0, nullptr, nullptr, nullptr, 0, partial, w.fs, f, k, alpha,
+                                     p_drop, seed, s);
+        continue;
+      }
+      rc = dev_err(hipStreamWaitEvent(s, d->exchanged, 0));  // the remainder part
+      if (rc == APPNP_OK)
+        rc = appnp_step_split_shards(d->g, a, b, APPNP_SHARDS_LAST, mainb[cur], remb[cur], H,
+                                     ld_h, last ? nullptr : mainb[nxt], last ? nullptr : remb[nxt],
+                                     last ? Z : nullptr, ld_z, partial, w.fs, f, k, alpha, p_drop,
+                                     seed, s);
+    }
+    // the own shard's send: the last thing on xs of this exchange (s waits for it before the
+    // next exchange reuses the buffer, at no cost: it precedes that exchange on xs anyway)
+    if (rc == APPNP_OK) rc = dev_err(hipStreamWaitEvent(s, d->arrived[d->nranks - 1], 0));
+    if (rc == APPNP_OK && !last) rc = exchange(nxt);
+  }
+  return rc;
+}
+
+// The same for whole rows (appnp_step_shards), the iterate in [P S, ld] buffers.
+int propagate_rows_pipelined(appnp_dist* d, const WsLayout& w, const void* H, int64_t ld_h,
+                             void* Z, int64_t ld_z, int64_t f, int K, float alpha, float p_drop,
+                             uint64_t seed, char* base, hipStream_t s) {
+  char* buf[2] = {base, base + w.buf_bytes};
+  float* partial = reinterpret_cast<float*>(base + w.partial_off);
+  const size_t row_bytes = (size_t)(w.ld * 4);
+  const size_t shard_bytes = (size_t)d->shard * row_bytes;
+  const int64_t rows = d->hi - d->lo;
+  auto own = [&](char* b) { return b + (size_t)d->lo * row_bytes; };
+  const int ri = d->rank;
+  int rc = dev_err(copy_rows(own(buf[0]), w.ld, H, ld_h, rows, f, 4, s));
+  if (rc == APPNP_OK) rc = exchange_shards(d, buf[0], shard_bytes, s);
+  for (int k = 0; k < K && rc == APPNP_OK; ++k) {
+    const bool last = k == K - 1;
+    const float* src = reinterpret_cast<const float*>(buf[k & 1]);
+    float* dst = last ? static_cast<float*>(Z) : reinterpret_cast<float*>(own(buf[(k + 1) & 1]));
+    const int64_t ld_dst = last ? ld_z : w.ld;
+    rc = appnp_step_shards(d->g, ri, ri + 1, APPNP_SHARDS_FIRST, src, w.ld, nullptr, 0, nullptr,
+                           0, partial, w.ld, f, k, alpha, p_drop, seed, s);
+    for (size_t i = 0; i < d->groups.size() && rc == APPNP_OK; ++i) {
+      const int a = d->groups[i].first, b = d->groups[i].second;
+      rc = dev_err(hipStreamWaitEvent(s, d->arrived[b - 1], 0));
+      const int mode = i + 1 < d->groups.size() ? APPNP_SHARDS_ACC : APPNP_SHARDS_LAST;
+      if (rc == APPNP_OK)
+        rc = appnp_step_shards(d->g, a, b, mode, src, w.ld, static_cast<const float*>(H), ld_h,
+                               dst, ld_dst, partial, w.ld, f, k, alpha, p_drop, seed, s);
+    }
+    if (rc == APPNP_OK) rc = dev_err(hipStreamWaitEvent(s, d->arrived[d->nranks - 1], 0));
+    if (rc == APPNP_OK && !last) rc = exchange_shards(d, buf[(k + 1) & 1], shard_bytes, s);
+  }
+  return rc;
+}
+
 // rows x (f elements) between two row-major matrices with leading dimensions in elements
 hipError_t copy_rows(void* dst, int64_t ld_dst, const void* src, int64_t ld_src, int64_t rows,
                      int64_t f, int64_t es, hipStream_t s) {
@@ -219,22 +363,37 @@ hipError_t copy_rows(void* dst, int64_t ld_dst, const void* src, int64_t ld_src,
                           (size_t)(f * es), (size_t)rows, hipMemcpyDeviceToDevice, s);
 }
 
-// RCCL, resolved at first use (appnp_allgather_rccl)
+// RCCL, resolved at first use (appnp_allgather_rccl, appnp_bcast_rccl)
 typedef int (*nccl_allgather_t)(const void*, void*, size_t, int, void*, hipStream_t);
+typedef int (*nccl_bcast_t)(const void*, void*, size_t, int, int, void*, hipStream_t);
 
-nccl_allgather_t rccl_allgather() {
-  static nccl_allgather_t fn = [] {
+void* rccl_handle() {
+  static void* h = [] {
     const char* env = std::getenv("APPNP_RCCL_LIB");
-    void* h = nullptr;
+    void* x = nullptr;
     if (env && *env) {
-      h = dlopen(env, RTLD_NOW | RTLD_LOCAL);
+      x = dlopen(env, RTLD_NOW | RTLD_LOCAL);
     } else {
       // the copy already in the process (PyTorch's), so its communicators are valid here
-      h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
-      if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+      x = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+      if (!x) x = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
     }
-    return h ? reinterpret_cast<nccl_allgather_t>(dlsym(h, "ncclAllGather")) : nullptr;
+    return x;
   }();
+  return h;
+}
+
+nccl_allgather_t rccl_allgather() {
+  static nccl_allgather_t fn = rccl_handle() ? reinterpret_cast<nccl_allgather_t>(
+                                                   dlsym(rccl_handle(), "ncclAllGather"))
+                                             : nullptr;
+  return fn;
+}
+
+nccl_bcast_t rccl_bcast() {
+  static nccl_bcast_t fn =
+      rccl_handle() ? reinterpret_cast<nccl_bcast_t>(dlsym(rccl_handle(), "ncclBroadcast"))
+                    : nullptr;
   return fn;
 }
 
@@ -341,12 +500,17 @@ int appnp_dist_propagate(appnp_dist* d, const void* H, int64_t ld_h, void* Z, in
       lz = w.f4;
     }
     if (rc == APPNP_OK)
-      rc = propagate_split_rows(d, w, h, lh, z, lz, f, K, alpha, p_drop, seed, base, s);
+      rc = (d->bcast && w.fs > 0)
+               ? propagate_split_rows_pipelined(d, w, h, lh, z, lz, f, K, alpha, p_drop, seed,
+                                                base, s)
+               : propagate_split_rows(d, w, h, lh, z, lz, f, K, alpha, p_drop, seed, base, s);
     if (rc == APPNP_OK && stage_z) rc = dev_err(copy_rows(Z, ld_z, zs, w.f4, rows, f, 4, s));
     return rc;
   }
   if (!ws || ws_bytes < w.total) return APPNP_EINVAL;
   char* base = static_cast<char*>(ws);
+  if (d->bcast && dtype == APPNP_F32)
+    return propagate_rows_pipelined(d, w, H, ld_h, Z, ld_z, f, K, alpha, p_drop, seed, base, s);
   char* buf[2] = {base, base + w.buf_bytes};
   float* partial = d->overlap ? reinterpret_cast<float*>(base + w.partial_off) : nullptr;
   const size_t row_bytes = (size_t)(w.ld * es);
@@ -393,14 +557,54 @@ int appnp_dist_propagate(appnp_dist* d, const void* H, int64_t ld_h, void* Z, in
   return rc;
 }
 
+int appnp_dist_set_broadcast(appnp_dist* d, appnp_bcast_fn fn, void* ctx, void* stream) {
+  if (!d || !fn) return APPNP_EINVAL;
+  if (!d->overlap || d->nranks < 3) return APPNP_ENOTSUP;  // nothing to pipeline
+  if (d->poisoned != APPNP_OK) return d->poisoned;
+  int rc = appnp_graph_shard_offsets(d->g, d->nranks, d->shard, stream);
+  std::vector<hipEvent_t> ev((size_t)d->nranks, nullptr);
+  for (size_t r = 0; r < ev.size() && rc == APPNP_OK; ++r)
+    rc = dev_err(hipEventCreateWithFlags(&ev[r], hipEventDisableTiming));
+  if (rc != APPNP_OK) {
+    for (hipEvent_t e : ev)
+      if (e) (void)hipEventDestroy(e);
+    return rc;
+  }
+  for (hipEvent_t e : d->arrived) (void)hipEventDestroy(e);
+  d->arrived = ev;
+  d->groups = shard_groups(d->nranks, d->rank);
+  d->bcast = fn;
+  d->bctx = ctx;
+  return APPNP_OK;
+}
+
+int appnp_dist_pipeline_groups(const appnp_dist* d, int* lo, int* hi, int max, int* n_out) {
+  if (!d || !n_out) return APPNP_EINVAL;
+  *n_out = d->bcast ? (int)d->groups.size() : 0;
+  for (int i = 0; i < *n_out && i < max; ++i) {
+    if (lo) lo[i] = d->groups[i].first;
+    if (hi) hi[i] = d->groups[i].second;
+  }
+  return APPNP_OK;
+}
+
 void appnp_dist_destroy(appnp_dist* d) {
   if (!d) return;
   if (d->xs) (void)hipStreamSynchronize(d->xs);
+  for (hipEvent_t e : d->arrived) (void)hipEventDestroy(e);
   if (d->produced) (void)hipEventDestroy(d->produced);
   if (d->exchanged) (void)hipEventDestroy(d->exchanged);
   if (d->xs) (void)hipStreamDestroy(d->xs);
   appnp_graph_destroy(d->g);
   delete d;
+}
+
+int appnp_bcast_rccl(void* buf, size_t bytes, int root, int nranks, void* stream, void* ctx) {
+  if (!buf || !ctx || root < 0 || root >= nranks) return APPNP_EINVAL;
+  const nccl_bcast_t fn = rccl_bcast();
+  if (!fn) return APPNP_ENOTSUP;
+  // ncclChar = 0; in place (sendbuff == recvbuff); ncclSuccess = 0
+  return fn(buf, buf, bytes, 0, root, ctx, as_stream(stream)) == 0 ? APPNP_OK : APPNP_EDEVICE;
 }
 
 int appnp_allgather_rccl(void* buf, size_t shard_bytes, int rank, int nranks, void* stream,

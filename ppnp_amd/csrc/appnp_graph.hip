@@ -316,7 +316,7 @@ void graph_free(appnp_graph* g) {
   void* ptrs[] = {g->row_ptr, g->col, g->val, g->lrow_ptr, g->lcol, g->lval,
                   g->rrow_ptr, g->rcol, g->rval, g->dinv, g->t_row_ptr, g->t_col, g->t_val,
                   g->heavy, g->t_heavy, g->hub, g->t_hub, g->rb_off, g->rb_ent, g->rb_val, g->rb_cblk,
-                  g->rb_dl, g->rb_dr};
+                  g->rb_dl, g->rb_dr, g->sh_off};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   g->row_ptr = g->col = g->lrow_ptr = g->lcol = g->rrow_ptr = g->rcol = nullptr;
@@ -332,6 +332,59 @@ void graph_free(appnp_graph* g) {
   g->rb_dl = g->rb_dr = nullptr;
   g->rb_nb = g->rb_passes = 0;
   g->rb_total = 0;
+  g->sh_off = nullptr;
+  g->sh_n = 0;
+  g->sh_rows = 0;
+}
+
+// Shard offsets of the held rows (graph_build_shard_offsets): thread per row; its entries are
+// sorted by column, so each shard boundary is found by a binary search of the row
+__global__ __launch_bounds__(kBlock) void k_shard_offsets(const int32_t* __restrict__ rp,
+                                                          const int32_t* __restrict__ col,
+                                                          int64_t rows, int nshards,
+                                                          int64_t shard_rows,
+                                                          int32_t* __restrict__ off) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= rows) return;
+  const int32_t beg = rp[i], end = rp[i + 1];
+  off[i] = beg;
+  off[(int64_t)nshards * rows + i] = end;
+  for (int s = 1; s < nshards; ++s) {
+    const int64_t bound = (int64_t)s * shard_rows;  // first column of shard s
+    int32_t lo = beg, hi = end;                     // first entry with col >= bound
+    while (lo < hi) {
+      const int32_t mid = lo + (hi - lo) / 2;
+      if ((int64_t)col[mid] < bound) lo = mid + 1; else hi = mid;
+    }
+    off[(int64_t)s * rows + i] = lo;
+  }
+}
+
+int graph_build_shard_offsets(appnp_graph* g, int nshards, int64_t shard_rows, hipStream_t s) {
+  if (!g || nshards < 1 || nshards > 1024 || shard_rows < 1 ||
+      (int64_t)nshards * shard_rows < g->n)
+    return APPNP_EINVAL;
+  const int64_t rows = g->row_hi - g->row_lo;
+  if (g->sh_off && g->sh_n == nshards && g->sh_rows == shard_rows) return APPNP_OK;
+  int32_t* off = nullptr;
+  hipError_t e = hipMalloc(&off, std::max<int64_t>(1, (nshards + 1) * rows) * sizeof(int32_t));
+  if (e == hipSuccess && rows > 0) {
+    hipLaunchKernelGGL(k_shard_offsets, dim3((unsigned)((rows + kBlock - 1) / kBlock)),
+                       dim3(kBlock), 0, s, g->row_ptr, g->col, rows, nshards, shard_rows, off);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) {
+    if (off) (void)hipFree(off);
+    (void)hipGetLastError();
+    return (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) ? APPNP_ENOMEM
+                                                                       : APPNP_EDEVICE;
+  }
+  if (g->sh_off) (void)hipFree(g->sh_off);
+  g->sh_off = off;
+  g->sh_n = nshards;
+  g->sh_rows = shard_rows;
+  return APPNP_OK;
 }
 
 #define APPNP_TRY(expr)                                                         \

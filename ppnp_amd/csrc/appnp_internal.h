@@ -62,6 +62,11 @@ struct appnp_graph {
   int32_t rb_pf = 0, rb_pc = 0; // LDS sums of a row: rb_pf 16-B pieces + rb_pc floats, i.e. the
                                 // pass is sized for 4 rb_pf + rb_pc remainder columns
   int64_t rb_direct_lo = 0;     // held rows [rb_direct_lo, rows) are gathered directly (no group)
+  // shard offsets of the held rows (appnp_graph_shard_offsets): entries of held row i with a
+  // column in shard s ([s sh_rows, (s+1) sh_rows)) are sh_off[s rows + i] .. sh_off[(s+1) rows + i]
+  int32_t* sh_off = nullptr;    // [(sh_n + 1) * rows]
+  int32_t sh_n = 0;
+  int64_t sh_rows = 0;
   double near_frac = 0.0;       // off-diagonal entries within kNearRows of their row / nnz
   // remainder-pass launches enqueued on this graph (appnp_graph_source_block_layout): the path
   // witness the tests read
@@ -77,6 +82,7 @@ int graph_build(const int32_t* indptr, const int32_t* indices, const float* vals
                 int64_t nnz, int mode, int64_t row_lo, int64_t row_hi, int split,
                 hipStream_t s, appnp_graph* g);
 void graph_free(appnp_graph* g);
+int graph_build_shard_offsets(appnp_graph* g, int nshards, int64_t shard_rows, hipStream_t s);
 int graph_build_transpose(appnp_graph* g, hipStream_t s);
 int build_heavy(const int32_t* rp, int64_t rows, int32_t thr, hipStream_t s, int32_t** out,
                 int64_t* n_out);

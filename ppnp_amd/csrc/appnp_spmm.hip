@@ -141,6 +141,13 @@ __device__ __forceinline__ void epilogue(const StepArgs& a, int64_t row, int col
     frag_store<T, V, TAIL>(d, dv, rem);
   } else if constexpr (EPI == EPI_PARTIAL) {
     frag_store<float, V, TAIL>(static_cast<float*>(a.out) + row * a.ld_out + col0, y, rem);
+  } else if constexpr (EPI == EPI_ACCUM) {
+    float* o = static_cast<float*>(a.out) + row * a.ld_out + col0;
+    float pv[V];
+    frag_load<float, V, TAIL>(o, pv, rem, row + 1 < a.n_rows);
+#pragma unroll
+    for (int v = 0; v < V; ++v) y[v] += pv[v];
+    frag_store<float, V, TAIL>(o, y, rem);
   } else {  // EPI_FINISH
     float pv[V];
     frag_load<float, V, TAIL>(static_cast<const float*>(a.aux) + row * a.ld_aux + col0, pv, rem,
@@ -174,7 +181,7 @@ __device__ __forceinline__ void wave_row(const StepArgs& a, int64_t row, int lan
   const bool fact = rem > 0;
   const T* __restrict__ zin = static_cast<const T*>(a.zin);
   const int beg = a.row_ptr[row];
-  const int end = a.row_ptr[row + 1];
+  const int end = row_end_of(a, row);
   float hv[V];
   if (sub == 0 && fact) load_h<T, V, EPI, TAIL>(a, row, col0, hv, rem);
   float acc[V];
@@ -293,7 +300,7 @@ __global__ __launch_bounds__(kBlock) void k_step_narrow(StepArgs a) {
     const int64_t row = rb + sub;
     if (row >= a.n_rows) continue;
     const int beg = a.row_ptr[row];
-    const int end = a.row_ptr[row + 1];
+    const int end = row_end_of(a, row);
     if (a.heavy && end - beg > a.heavy_thr) continue;
     float hv[V];
     if (fact) load_h<T, V, EPI, TAIL>(a, row, col0, hv, rem);
@@ -508,6 +515,7 @@ hipError_t launch_step(int dtype, int epi, int V, const StepArgs& a_in, hipStrea
       case EPI_BWD: return launch_v<float, EPI_BWD>(V, G, wide, uw, un, grid, a, s);
       case EPI_PARTIAL: return launch_v<float, EPI_PARTIAL>(V, G, wide, uw, un, grid, a, s);
       case EPI_FINISH: return launch_v<float, EPI_FINISH>(V, G, wide, uw, un, grid, a, s);
+      case EPI_ACCUM: return launch_v<float, EPI_ACCUM>(V, G, wide, uw, un, grid, a, s);
     }
   } else {
     switch (epi) {

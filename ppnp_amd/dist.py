@@ -207,6 +207,25 @@ class _TorchComm:
             full.copy_(host)
         return None
 
+    supports_broadcast = True
+
+    def broadcast_rows(self, full: torch.Tensor, shard_rows: int, root: int, async_op: bool):
+        """In-place broadcast of row shard ``root`` (a row-group index) of ``full`` from its
+        owner to the column group: one step of the pipelined exchange, whose R broadcasts land
+        one shard at a time (roots in the same order on every rank).  RCCL: an async work whose
+        wait() orders the caller's stream after it; gloo: synchronous, through host memory."""
+        if self.layout.rows == 1:
+            return None
+        view = full[root * shard_rows:(root + 1) * shard_rows]
+        src = self.ci * self.layout.rows + root  # global rank of that row group's member
+        if self.backend == "nccl":
+            return dist.broadcast(view, src=src, group=self.group, async_op=async_op)
+        host = view.detach().to("cpu", copy=True) if view.is_cuda else view
+        dist.broadcast(host, src=src, group=self.group)
+        if view.is_cuda:
+            view.copy_(host)
+        return None
+
 
 def _pieces(rows: int, parts: int):
     """Row bounds of ``parts`` near-equal pieces of a shard of ``rows`` rows."""
@@ -402,9 +421,39 @@ class NullComm:
     """No exchange (emulation of one rank on one GPU; the gathered rows keep stale data)."""
 
     name = "none"
+    supports_broadcast = True
 
     def all_gather_rows(self, full, shard_rows, async_op):
         return None
+
+    def broadcast_rows(self, full, shard_rows, root, async_op):
+        return None
+
+
+def shard_groups(R: int, ri: int):
+    """The pipelined step's groups of REMOTE source shards for row group ri of R: shard ranges
+    [a, b) in arrival order (the exchange broadcasts roots 0 .. R-1 in turn), sized 1, 2, 4, ...
+    from the last to arrive backwards (7 remote shards: 4 + 2 + 1), and cut where a group would
+    span the rank's own shard, whose rows are not exchanged to it.  Each group's product runs as
+    soon as its last shard has landed, so after the exchange only the last group's -- one
+    shard's -- compute is left, for log2(R) extra passes over the fp32 partial instead of R - 2."""
+    arrival = [s for s in range(R) if s != ri]
+    sizes, left, sz = [], len(arrival), 1
+    while left > 0:
+        take = min(sz, left)
+        sizes.append(take)
+        left -= take
+        sz *= 2
+    groups, pos = [], 0
+    for take in reversed(sizes):
+        chunk = arrival[pos:pos + take]
+        pos += take
+        start = chunk[0]
+        for a, b in zip(chunk, chunk[1:] + [None]):
+            if b is None or b != a + 1:
+                groups.append((start, a + 1))
+                start = b
+    return groups
 
 
 class PartitionedAPPNP:
@@ -432,12 +481,16 @@ class PartitionedAPPNP:
     @classmethod
     def create(cls, indptr, indices, n, H, K, alpha, device, layout: Layout | None = None,
                overlap=False, data=None, mode="sym", comm=None, step_fn=None, graph_fn=None,
-               p_drop=0.0, seed=0, rank=None, world=None, exchange="multipath"):
+               p_drop=0.0, seed=0, rank=None, world=None, exchange="multipath", pipeline=None):
         """rank / world override the process group's (single-GPU emulation of one rank of a
         larger layout, with a ``NullComm``: measures that rank's kernel time only).
         exchange: 'multipath' (MultipathComm, R x C layouts with C > 1) or 'group' (one RCCL
         all-gather per column group); a pure row layout always uses the all-gather, or, with
-        'native', the library's own loop (NativeRowRunner over appnp_dist_*)."""
+        'native', the library's own loop (NativeRowRunner over appnp_dist_*).
+        pipeline: with overlap and R >= 3 row groups, exchange the iterate by R broadcasts, one
+        row shard each, and run the remote product one group of arrived shards at a time
+        (``shard_groups``), so only the last shard's compute follows the exchange (VERDICT r5
+        #2).  None: whenever it applies (the exchange supports broadcasts)."""
         if rank is None:
             rank = dist.get_rank() if dist.is_initialized() else 0
         if world is None:
@@ -449,7 +502,8 @@ class PartitionedAPPNP:
             if layout.cols != 1 or comm is not None or step_fn is not None or graph_fn is not None:
                 raise ValueError("exchange='native' runs a pure row layout on the HIP path")
             return NativeRowRunner(indptr, indices, n, H, K, alpha, device, overlap=overlap,
-                                   mode=mode, data=data, p_drop=p_drop, seed=seed)
+                                   mode=mode, data=data, p_drop=p_drop, seed=seed,
+                                   pipeline=pipeline)
         ri, ci = layout.coords(rank)
         f = int(H.shape[1])
         lo, hi, shard = row_range(n, layout.rows, ri)
@@ -519,6 +573,24 @@ class PartitionedAPPNP:
                         for _ in range(2)]
             obj.zout = torch.zeros(max(hi - lo, 0), ld, dtype=torch.float32, device=device)
         obj.exchange = getattr(comm, "name", "group")
+        R = layout.rows
+        can = (overlap and R >= 3 and getattr(comm, "supports_broadcast", False)
+               and (split is None or split[0] > 0))
+        if pipeline and not can:
+            raise ValueError("pipeline needs overlap, >= 3 row groups and a broadcast exchange")
+        obj.pipeline = bool(can if pipeline is None else pipeline)
+        obj.groups = shard_groups(R, ri) if obj.pipeline else None
+        if obj.pipeline:
+            if hasattr(graph, "shard_offsets"):
+                graph.shard_offsets(R, shard)
+            else:
+                from .ops import shard_offsets
+
+                shard_offsets(graph, R, shard)
+            if obj.partial is None:
+                w = split[0] if split is not None else ld
+                obj.partial = torch.zeros(max(hi - lo, 0), max(w, 4), dtype=torch.float32,
+                                          device=device)
         return obj
 
     @property
@@ -552,12 +624,74 @@ class PartitionedAPPNP:
                     works.append(w)
         return works
 
+    def _broadcast_shards(self, full):
+        """The pipelined exchange of one iterate (main part on the split layout): R in-place
+        broadcasts, root 0 .. R-1 in turn; handle per shard (None when synchronous)."""
+        return [self.comm.broadcast_rows(full, self.shard, r, async_op=True)
+                for r in range(self.layout.rows)]
+
+    @staticmethod
+    def _wait(handles, lo, hi):
+        for r in range(lo, hi):
+            if handles[r] is not None:
+                handles[r].wait()
+                handles[r] = None
+
+    def _run_split_pipelined(self):
+        """``_run_split`` with the pipelined exchange: the remainder part is all-gathered first
+        (it lands before the main part's shards), the main part travels by R broadcasts, and the
+        main product runs FIRST on the own shard, then one launch per group of arrived shards
+        (appnp_step_split_shards), the last of which finishes the rows and runs the remainder
+        pass."""
+        from .ops import split_copy, step_split_shards
+
+        K, w, g, R = self.K, self.width, self.graph, self.layout.rows
+        ri = self.layout.coords(self.rank)[0]
+        H = self.H[:, :w]
+        kw = dict(p_drop=self.p_drop, seed=self.seed)
+        part = self.partial[:, :self.split[0]]
+        split_copy(g, H, self.smain[0], self.srem[0])
+
+        def exchange(b):
+            rem = self.comm.all_gather_rows(self.srem[b], self.shard, async_op=True)
+            return rem, self._broadcast_shards(self.smain[b])
+
+        rem, shards = exchange(0)
+        for k in range(K):
+            cur, nxt = k & 1, (k & 1) ^ 1
+            last = k == K - 1
+            zin = (self.smain[cur], self.srem[cur])
+            step_split_shards(g, ri, ri + 1, _lib.SHARDS_FIRST, zin[0], None, None, w, k,
+                              self.alpha, partial=part, **kw)
+            for i, (a, b) in enumerate(self.groups):
+                self._wait(shards, a, b)
+                if i + 1 < len(self.groups):
+                    step_split_shards(g, a, b, _lib.SHARDS_ACC, zin[0], None, None, w, k,
+                                      self.alpha, partial=part, **kw)
+                    continue
+                if rem is not None:
+                    rem.wait()
+                    rem = None
+                step_split_shards(g, a, b, _lib.SHARDS_LAST, zin[0], zin[1], H, w, k,
+                                  self.alpha, out_main=None if last else self.smain[nxt],
+                                  out_rem=None if last else self.srem[nxt],
+                                  Z=self.zout[:, :w] if last else None, partial=part, **kw)
+            # the own shard's send is the only handle left: it precedes the next exchange on
+            # the communicator's stream, so waiting for it here costs nothing
+            self._wait(shards, 0, R)
+            if not last:
+                rem, shards = exchange(nxt)
+        self.out = self.zout[:, :w]
+        return self.out
+
     def _run_split(self):
         """The row-group loop on the split layout (appnp_step_split): the main columns gather
         whole lines (local / remote parts with overlap), the remainder columns run the
         L2-blocked pass once the exchange of the iterate has landed."""
         from .ops import split_copy, step_split
 
+        if self.pipeline:
+            return self._run_split_pipelined()
         K, w, g = self.K, self.width, self.graph
         fs, _ = self.split
         H = self.H[:, :w]
@@ -601,6 +735,8 @@ class PartitionedAPPNP:
             return self.out
         if self.split is not None:
             return self._run_split()
+        if self.pipeline:
+            return self._run_pipelined()
         if R == 1 and self.step_fn is _hip_step:
             # column layout: this rank holds every row of its slab, so the K iterations are one
             # appnp_propagate call (no per-iteration host work between the launches)
@@ -644,6 +780,35 @@ class PartitionedAPPNP:
         return self.out
 
 
+    def _run_pipelined(self):
+        """The row loop with the pipelined exchange (whole rows): every iterate travels by R
+        broadcasts, one row shard each; the product runs FIRST on the own shard (complete at
+        once), then ACC per group of arrived remote shards, the last group LAST (partial +
+        alpha H into the rank's rows)."""
+        K, R, w = self.K, self.layout.rows, self.width
+        lo, hi = self.lo, self.hi
+        ri = self.layout.coords(self.rank)[0]
+        cur = self.bufs[0]
+        cur[lo:hi].copy_(self.H)
+        shards = self._broadcast_shards(cur)
+        nxt_i = 1
+        for k in range(K):
+            dst = self.bufs[nxt_i]
+            out_rows = dst[lo:hi]
+            self.step_fn(self, cur, out_rows, k, ("shards", ri, ri + 1, _lib.SHARDS_FIRST))
+            for i, (a, b) in enumerate(self.groups):
+                self._wait(shards, a, b)
+                mode = _lib.SHARDS_ACC if i + 1 < len(self.groups) else _lib.SHARDS_LAST
+                self.step_fn(self, cur, out_rows, k, ("shards", a, b, mode))
+            self._wait(shards, 0, R)  # the own shard's send (see _run_split_pipelined)
+            if k < K - 1:
+                shards = self._broadcast_shards(dst)
+            cur = dst
+            nxt_i ^= 1
+        self.out = cur[lo:hi, :w]
+        return self.out
+
+
 def agree_split(split, device, group=None):
     """The split layout every rank of the (default) process group takes: this rank's ``split``
     -- (fs, remainder width) or None -- if every rank found the SAME (fs, width), else None
@@ -673,6 +838,15 @@ def _hip_step(runner: PartitionedAPPNP, src, out_rows, k, part):
     w = runner.width
     Zin = src[:, :w] if src.shape[0] == runner.graph.n else src[: runner.graph.n, :w]
     H = runner.H[:, :w]
+    if isinstance(part, tuple):  # ("shards", s_lo, s_hi, mode): a pipelined step
+        from .ops import step_shards
+
+        _, a, b, mode = part
+        to_partial = mode in (_lib.SHARDS_FIRST, _lib.SHARDS_ACC)
+        step_shards(runner.graph, a, b, mode, Zin, None if to_partial else H,
+                    None if to_partial else out_rows[:, :w], runner.partial[:, :w], k,
+                    runner.alpha, p_drop=runner.p_drop, seed=runner.seed)
+        return
     if part == _lib.PART_LOCAL:
         step(runner.graph, Zin, None, runner.partial[:, :w], k, runner.alpha,
              part=_lib.PART_LOCAL, p_drop=runner.p_drop, seed=runner.seed)
@@ -697,10 +871,13 @@ class NativeRowAPPNP:
     and runs it with the same arguments."""
 
     def __init__(self, indptr, indices, n, device, overlap=True, mode="sym", data=None,
-                 exchange=None, rank=None, world=None, features=None, dtype=torch.float32):
+                 exchange=None, rank=None, world=None, features=None, dtype=torch.float32,
+                 pipeline=None):
         """features: the F the engine will propagate; when fp32 rows of that width split
         (graph.remainder_width), the held rows get a source-blocked copy and the engine runs the
-        split layout (appnp_step_split)."""
+        split layout (appnp_step_split).  pipeline: the engine's pipelined exchange
+        (appnp_dist_set_broadcast: one broadcast per row shard, the product per group of
+        arrived shards); None: whenever it applies (overlap, >= 3 ranks)."""
         import ctypes as C
 
         from .graph import source_block_flags
@@ -741,6 +918,38 @@ class NativeRowAPPNP:
         _lib.check("appnp_dist_rows", lib.appnp_dist_rows(h, C.byref(lo), C.byref(hi),
                                                           C.byref(shard)))
         self.n, self.lo, self.hi, self.shard = n, lo.value, hi.value, shard.value
+        can = bool(overlap) and self.world >= 3
+        if pipeline and not can:
+            raise ValueError("pipeline needs overlap and >= 3 ranks")
+        self.pipeline = bool(can if pipeline is None else pipeline)
+        self._bfn = None
+        if self.pipeline:
+            if self.exchange == "rccl":
+                bfn = _lib.BCAST_FN(C.cast(lib.appnp_bcast_rccl, C.c_void_p).value)
+            else:
+                bfn = _lib.BCAST_FN(self._gloo_bcast)
+            self._bfn = bfn  # the ctypes callback must outlive the handle
+            _lib.check("appnp_dist_set_broadcast", lib.appnp_dist_set_broadcast(
+                h, bfn, ctx, stream))
+        n_g = C.c_int(0)
+        lo_g, hi_g = (C.c_int * 64)(), (C.c_int * 64)()
+        _lib.check("appnp_dist_pipeline_groups",
+                   lib.appnp_dist_pipeline_groups(h, lo_g, hi_g, 64, C.byref(n_g)))
+        self.groups = [(lo_g[i], hi_g[i]) for i in range(min(n_g.value, 64))]
+
+    def _gloo_bcast(self, buf, nbytes, root, nranks, stream, ctx):
+        self.gloo_bcasts = getattr(self, "gloo_bcasts", 0) + 1  # tests: broadcasts made
+        try:
+            torch.cuda.synchronize(self.device)
+            off = buf - self._ws.data_ptr()
+            view = self._ws[off:off + nbytes]
+            host = view.cpu()
+            dist.broadcast(host, src=root)
+            view.copy_(host)
+            torch.cuda.synchronize(self.device)
+            return 0
+        except Exception:  # noqa: BLE001 -- no Python exception may cross the C frame
+            return _lib.APPNP_EDEVICE
 
     def _gloo_allgather(self, buf, shard_bytes, rank, nranks, stream, ctx):
         self.gloo_calls = getattr(self, "gloo_calls", 0) + 1  # tests: exchanges the engine made
@@ -826,9 +1035,11 @@ class NativeRowRunner:
     exchange = "native"
 
     def __init__(self, indptr, indices, n, H, K, alpha, device, overlap=True, mode="sym",
-                 data=None, p_drop=0.0, seed=0):
+                 data=None, p_drop=0.0, seed=0, pipeline=None):
         self.engine = NativeRowAPPNP(indptr, indices, n, device, overlap=overlap, mode=mode,
-                                     data=data, features=int(H.shape[1]), dtype=H.dtype)
+                                     data=data, features=int(H.shape[1]), dtype=H.dtype,
+                                     pipeline=pipeline)
+        self.pipeline = self.engine.pipeline
         self.layout = Layout(self.engine.world, 1)
         self.rank = self.engine.rank
         self.overlap = bool(overlap and self.engine.world > 1)

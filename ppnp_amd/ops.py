@@ -156,6 +156,50 @@ def step(graph: Graph, Zin: torch.Tensor, H: torch.Tensor, out: torch.Tensor, k:
     return out
 
 
+def shard_offsets(graph: Graph, nshards: int, shard_rows: int) -> None:
+    """The held rows' entries grouped by source shard (``appnp_graph_shard_offsets``), for the
+    pipelined row steps ``step_shards`` / ``step_split_shards``."""
+    with torch.cuda.device(graph.device):
+        rc = _lib.load().appnp_graph_shard_offsets(graph.handle, int(nshards), int(shard_rows),
+                                                   _stream(graph.device))
+    _lib.check("appnp_graph_shard_offsets", rc)
+
+
+def step_shards(graph: Graph, s_lo: int, s_hi: int, mode: int, Zin: torch.Tensor,
+                H: torch.Tensor | None, out: torch.Tensor | None, partial: torch.Tensor | None,
+                k: int, alpha: float, p_drop: float = 0.0, seed: int = 0) -> None:
+    """One iteration's product over source shards [s_lo, s_hi) of the held rows
+    (``appnp_step_shards``): mode SHARDS_FIRST / _ACC into ``partial``, _LAST / _ONLY into
+    ``out`` (fp32; Zin holds all n rows)."""
+    _check_dense("Zin", Zin, graph, graph.n)
+    f = int(Zin.shape[1])
+    with torch.cuda.device(graph.device):
+        rc = _lib.load().appnp_step_shards(
+            graph.handle, int(s_lo), int(s_hi), int(mode), _vp(Zin), _ld(Zin), _vp(H),
+            _ld(H) if H is not None else 0, _vp(out), _ld(out) if out is not None else 0,
+            _vp(partial), _ld(partial) if partial is not None else 0, f, int(k), float(alpha),
+            float(p_drop), int(seed) & (2**64 - 1), _stream(graph.device))
+    _lib.check("appnp_step_shards", rc)
+
+
+def step_split_shards(graph: Graph, s_lo: int, s_hi: int, mode: int,
+                      zin_main: torch.Tensor | None, zin_rem: torch.Tensor | None,
+                      H: torch.Tensor | None, f: int, k: int, alpha: float,
+                      out_main: torch.Tensor | None = None, out_rem: torch.Tensor | None = None,
+                      Z: torch.Tensor | None = None, partial: torch.Tensor | None = None,
+                      p_drop: float = 0.0, seed: int = 0) -> None:
+    """``step_shards`` on the split layout (``appnp_step_split_shards``): the main columns take
+    the shard range and mode; _LAST / _ONLY then run the remainder pass."""
+    with torch.cuda.device(graph.device):
+        rc = _lib.load().appnp_step_split_shards(
+            graph.handle, int(s_lo), int(s_hi), int(mode), _vp(zin_main), _vp(zin_rem), _vp(H),
+            _ld(H) if H is not None else 0, _vp(out_main), _vp(out_rem), _vp(Z),
+            _ld(Z) if Z is not None else 0, _vp(partial),
+            _ld(partial) if partial is not None else 0, int(f), int(k), float(alpha),
+            float(p_drop), int(seed) & (2**64 - 1), _stream(graph.device))
+    _lib.check("appnp_step_split_shards", rc)
+
+
 def split_copy(graph: Graph, H: torch.Tensor, main: torch.Tensor | None,
                rem: torch.Tensor) -> None:
     """Z_0 of the split layout on the held rows (``appnp_split_copy``): H [held rows, F] into

@@ -47,6 +47,8 @@ def main():
                    help="every rank's split agreement fails after its exchange "
                         "(APPNP_DIST_TEST_AGREE_FAIL): the first call returns the error, later "
                         "calls return it again without exchanging (the poisoned handle)")
+    p.add_argument("--pipeline", default="auto", choices=["auto", "on", "off"],
+                   help="the engine's pipelined exchange (appnp_dist_set_broadcast)")
     a = p.parse_args()
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
@@ -79,7 +81,9 @@ def main():
     if rank == a.sb_oom_rank:
         os.environ["APPNP_SB_TEST_OOM"] = "1"
     runner = pdist.NativeRowAPPNP(indptr, indices, n, dev, overlap=a.overlap,
-                                  features=F if a.split else None, dtype=dtype)
+                                  features=F if a.split else None, dtype=dtype,
+                                  pipeline={"auto": None, "on": True,
+                                            "off": False}[a.pipeline])
     g = pdist._DistGraphInfo(C.c_void_p(_lib.load().appnp_dist_graph(runner._h)))
     before = (g.source_block_layout() or {}).get("launches", 0)
     if a.agree_fail:
@@ -140,12 +144,25 @@ def main():
         torch.cuda.synchronize()
         ok = ok and rc == 0 and torch.equal(buf, before)
         extra += f" rccl_callback rc={rc}"
+        # the pipelined exchange's RCCL broadcast: a one-rank in-place broadcast
+        rc = lib.appnp_bcast_rccl(C.c_void_p(buf.data_ptr()), buf.numel() * 4, 0, 1,
+                                  C.c_void_p(torch.cuda.current_stream(dev).cuda_stream),
+                                  C.c_void_p(comm))
+        torch.cuda.synchronize()
+        ok = ok and rc == 0 and torch.equal(buf, before)
+        extra += f" rccl_bcast rc={rc}"
         # torch's own in-place all-gather on the data-path group (the _TorchComm call)
         full = torch.arange(64, dtype=torch.float32, device=dev)
         dist.all_gather_into_tensor(full, full[:64], group=pdist.data_group())
         torch.cuda.synchronize()
         ok = ok and torch.equal(full, torch.arange(64, dtype=torch.float32, device=dev))
         ok = ok and runner.exchange == "rccl"
+    if runner.pipeline:
+        # one broadcast per row shard and exchanged iterate (Z_0 .. Z_{K-1}), the product per
+        # group of arrived shards
+        bc = getattr(runner, "gloo_bcasts", None)
+        ok = ok and (bc is None or bc == K * world) and len(runner.groups) >= 1
+        extra += f" pipeline=True groups={runner.groups} bcasts={bc}"
     runner.close()
     print(f"[dist_capi] rank {rank}/{world} backend={dist.get_backend()} "
           f"exchange={runner.exchange} overlap={a.overlap} dtype={a.dtype} p_drop={a.p_drop} "

@@ -59,6 +59,9 @@ def main():
                    help="with --oracle-torch: rank 0 alone runs the oracle and sends every rank "
                         "its block (gloo point to point), instead of every rank running it -- "
                         "8 products-scale fp64 oracles would not fit the box's CPU share")
+    p.add_argument("--pipeline", default="auto", choices=["auto", "on", "off"],
+                   help="the pipelined exchange (one broadcast per row shard, the product per "
+                        "group of arrived shards): auto = whenever it applies")
     p.add_argument("--expect-split", type=int, default=None,
                    help="fail unless the rank's remainder columns (split rows) equal this")
     p.add_argument("--sb-oom-rank", type=int, default=-1,
@@ -94,7 +97,9 @@ def main():
         os.environ["APPNP_SB_TEST_OOM"] = "1"
     runner = pdist.PartitionedAPPNP.create(indptr, indices, a.n, H, a.K, a.alpha, dev,
                                            layout=layout, overlap=a.overlap,
-                                           p_drop=a.p_drop, seed=5, exchange=a.exchange)
+                                           p_drop=a.p_drop, seed=5, exchange=a.exchange,
+                                           pipeline={"auto": None, "on": True,
+                                                     "off": False}[a.pipeline])
     Z = runner.run()
     torch.cuda.synchronize()
     if a.oracle_torch and a.oracle_rank0:
@@ -131,6 +136,7 @@ def main():
         ok = ok and runner.remainder_cols == a.expect_split
     print(f"[dist_worker] rank {rank}/{world} backend={dist.get_backend()} layout={layout} "
           f"overlap={runner.overlap} exchange={runner.exchange} split_cols={runner.remainder_cols} "
+          f"pipeline={runner.pipeline} "
           f"rows [{runner.lo},{runner.hi}) "
           f"cols [{runner.f_lo},"
           f"{runner.f_hi}) reference={'oracle' if a.oracle or a.oracle_torch else 'hip'} "

@@ -149,6 +149,9 @@ class _StubGraph:
     def __init__(self, n, lo, hi):
         self.n, self.rows, self.nnz_hat = n, hi - lo, 10 * (hi - lo)
 
+    def shard_offsets(self, nshards, shard_rows):  # the pipelined row steps' shard ranges
+        pass
+
 
 def _noop_step(runner, src, out_rows, k, part):
     pass

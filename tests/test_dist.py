@@ -34,6 +34,16 @@ class _FakeGraph:
             self.remote = sp.csr_matrix((coo.data[~loc], (coo.row[~loc], coo.col[~loc])),
                                         shape=shape)
 
+    def shard_offsets(self, nshards, shard_rows):
+        """The pipelined steps' source shards (appnp_graph_shard_offsets): the rows' entries by
+        the shard of their column."""
+        self.shard_rows = shard_rows
+
+    def shard_part(self, s_lo, s_hi):
+        coo = self.rows_csr.tocoo()
+        m = (coo.col >= s_lo * self.shard_rows) & (coo.col < s_hi * self.shard_rows)
+        return sp.csr_matrix((coo.data[m], (coo.row[m], coo.col[m])), shape=self.rows_csr.shape)
+
 
 def _oracle_step(runner, src, out_rows, k, part):
     from ppnp_amd import _lib
@@ -43,6 +53,20 @@ def _oracle_step(runner, src, out_rows, k, part):
     Zin = src[: g.n, :w].double().numpy()
     H = runner.H[:, :w].double().numpy()
     a = 1.0 - runner.alpha
+    if isinstance(part, tuple):  # a pipelined step over source shards [s_lo, s_hi)
+        _, s_lo, s_hi, mode = part
+        y = a * (g.shard_part(s_lo, s_hi) @ Zin)
+        P = runner.partial[:, :w].double().numpy()
+        if mode == _lib.SHARDS_FIRST:
+            runner.partial[:, :w] = torch.from_numpy(y).float()
+        elif mode == _lib.SHARDS_ACC:
+            runner.partial[:, :w] = torch.from_numpy(y + P).float()
+        elif mode == _lib.SHARDS_LAST:
+            out_rows[:, :w] = torch.from_numpy(y + P + runner.alpha * H).float()
+        else:
+            out_rows[:, :w] = torch.from_numpy(y + runner.alpha * H).float()
+        runner.shard_steps = getattr(runner, "shard_steps", 0) + 1
+        return
     if part == _lib.PART_LOCAL:
         runner.partial[:, :w] = torch.from_numpy(a * (g.local @ Zin)).float()
     elif part == _lib.PART_REMOTE:
@@ -52,7 +76,8 @@ def _oracle_step(runner, src, out_rows, k, part):
         out_rows[:, :w] = torch.from_numpy(a * (g.rows_csr @ Zin) + runner.alpha * H).float()
 
 
-def _worker(rank, world, init, layout_spec, overlap, q, exchange="multipath", f=F):
+def _worker(rank, world, init, layout_spec, overlap, q, exchange="multipath", f=F,
+            pipeline=None):
     dist.init_process_group("gloo", init_method=init, rank=rank, world_size=world)
     try:
         from ppnp_amd.dist import Layout, PartitionedAPPNP
@@ -64,8 +89,10 @@ def _worker(rank, world, init, layout_spec, overlap, q, exchange="multipath", f=
         runner = PartitionedAPPNP.create(
             None, None, N, H, K, ALPHA, "cpu", layout=layout, overlap=overlap,
             graph_fn=lambda lo, hi, ov: _FakeGraph(a_hat, lo, hi, ov), step_fn=_oracle_step,
-            exchange=exchange)
+            exchange=exchange, pipeline=pipeline)
         Z = runner.run()
+        if pipeline:  # the pipelined schedule ran: FIRST + one launch per shard group per step
+            assert runner.pipeline and runner.shard_steps == K * (1 + len(runner.groups))
         ref = O.appnp_propagate(a_hat, H.numpy(), K, ALPHA)
         sub = ref[runner.lo:runner.hi, runner.f_lo:runner.f_hi]
         err = float(np.abs(Z.double().numpy() - sub).max()) if sub.size else 0.0
@@ -99,10 +126,11 @@ def _rendezvous():
     # relayed exchange packs each origin's piece at its own column group's width
     (4, "2x2", False, "multipath", 73), (4, "2x2", True, "multipath", 73),
     (4, "2x2", True, "group", 73)])
-def test_partitioned_matches_oracle(world, layout, overlap, exchange, f):
+def test_partitioned_matches_oracle(world, layout, overlap, exchange, f, pipeline=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    mp.start_processes(_worker, args=(world, _rendezvous(), layout, overlap, q, exchange, f),
+    mp.start_processes(_worker, args=(world, _rendezvous(), layout, overlap, q, exchange, f,
+                                      pipeline),
                        nprocs=world, join=True, start_method="spawn")
     res = sorted(q.get() for _ in range(world))
     covered = np.zeros((N, f), dtype=bool)
@@ -110,6 +138,33 @@ def test_partitioned_matches_oracle(world, layout, overlap, exchange, f):
         assert err < 1e-5, (rank, err)
         covered[lo:hi, flo:fhi] = True
     assert covered.all()  # every (row, feature) of Z_K is produced exactly by some rank
+
+
+@pytest.mark.parametrize("world,layout,exchange", [
+    (3, "row", "group"), (4, "row", "group"), (8, "row", "group"), (8, "4x2", "group")])
+def test_pipelined_row_steps_match_oracle(world, layout, exchange):
+    """the iterate travels by R broadcasts, one row shard each, and the
+    remote product runs per group of arrived shards (FIRST on the own shard, ACC, LAST); every
+    rank's block still matches the oracle at world 3 / 4 / 8, pure rows and 4 x 2."""
+    test_partitioned_matches_oracle(world, layout, True, exchange, F, pipeline=True)
+
+
+def test_shard_groups():
+    """Groups of remote shards in arrival order, sized 1, 2, 4 from the last, never spanning
+    the own shard; every remote shard exactly once."""
+    from ppnp_amd.dist import shard_groups
+
+    assert shard_groups(2, 0) == [(1, 2)] and shard_groups(2, 1) == [(0, 1)]
+    assert shard_groups(8, 0) == [(1, 5), (5, 7), (7, 8)]
+    assert shard_groups(8, 7) == [(0, 4), (4, 6), (6, 7)]
+    assert shard_groups(8, 3) == [(0, 3), (4, 5), (5, 7), (7, 8)]
+    for R in range(2, 17):
+        for ri in range(R):
+            g = shard_groups(R, ri)
+            covered = [s for a, b in g for s in range(a, b)]
+            assert covered == [s for s in range(R) if s != ri]
+            assert all(not (a <= ri < b) for a, b in g)
+            assert g[-1][1] - g[-1][0] == 1  # only one shard's compute after the exchange
 
 
 def test_layout_helpers():

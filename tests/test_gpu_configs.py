@@ -224,10 +224,13 @@ def _free_port():
 
 
 @pytest.mark.parametrize("ranks,extra", [(2, []), (2, ["--overlap"]), (4, []),
-                                         (4, ["--overlap"])])
+                                         (4, ["--overlap", "--pipeline", "off"]),
+                                         (4, ["--overlap"]), (3, ["--overlap", "--p-drop", "0.2"])])
 def test_arxiv_row_partition_matches_oracle(ranks, extra):
     """Config 4 row-partitioned: each rank's block of Z_K (real HIP kernels, gloo exchange
-    staged through host memory since the ranks share one GPU) against the float64 oracle."""
+    staged through host memory since the ranks share one GPU) against the float64 oracle.
+    From 3 ranks on, overlap pipelines the exchange (one broadcast per row shard, the product
+    per group of arrived shards: appnp_step_shards) unless switched off."""
     env = dict(os.environ, PPNP_DIST_BACKEND="gloo", PYTHONPATH=ROOT,
                OMP_NUM_THREADS="2")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
@@ -238,6 +241,8 @@ def test_arxiv_row_partition_matches_oracle(ranks, extra):
     assert proc.returncode == 0, proc.stdout[-3000:] + proc.stderr[-3000:]
     res = _rank_results(proc.stdout, "dist_worker")
     assert res == {r: "OK" for r in range(ranks)}, proc.stdout[-4000:]
+    piped = ranks >= 3 and "--overlap" in extra and "off" not in extra
+    assert proc.stdout.count("pipeline=True") == (ranks if piped else 0), proc.stdout[-4000:]
 
 
 @pytest.mark.parametrize("ranks", [2, 4])
@@ -352,11 +357,14 @@ def test_bench_rccl_refused_still_prints_the_column_line():
 
 @pytest.mark.parametrize("ranks,extra", [
     (2, ["--overlap"]), (2, []), (3, ["--overlap", "--p-drop", "0.3"]),
+    (3, ["--overlap", "--pipeline", "off"]),
     (2, ["--dtype", "bf16"]), (4, ["--workload", "arxiv-synth", "--overlap"])])
 def test_native_row_engine_matches_single_gpu(ranks, extra):
     """The library's own row-partitioned loop (appnp_dist_create / appnp_dist_propagate: the
     C engine of SURVEY.md 8(b)) over 2-4 ranks sharing the GPU, with the exchange supplied
-    as a host-staged gloo callback, against the single-GPU appnp_propagate."""
+    as a host-staged gloo callback, against the single-GPU appnp_propagate.  From 3 ranks on,
+    overlap pipelines the exchange through a broadcast callback (appnp_dist_set_broadcast)
+    unless switched off."""
     env = dict(os.environ, PPNP_DIST_BACKEND="gloo", PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
            f"--nproc-per-node={ranks}", "--master-addr=127.0.0.1",
@@ -366,6 +374,8 @@ def test_native_row_engine_matches_single_gpu(ranks, extra):
     assert proc.returncode == 0, proc.stdout[-3000:] + proc.stderr[-3000:]
     res = _rank_results(proc.stdout, "dist_capi")
     assert res == {r: "OK" for r in range(ranks)}, proc.stdout[-4000:]
+    piped = ranks >= 3 and "--overlap" in extra and "off" not in extra
+    assert proc.stdout.count("pipeline=True") == (ranks if piped else 0), proc.stdout[-4000:]
 
 
 @pytest.mark.parametrize("backend", ["nccl", "gloo+nccl"])

@@ -1,6 +1,7 @@
 #!/usr/bin/env python
 """Time the adjoint (appnp_propagate_bwd) and the forward on a bench workload, per iteration,
-with HIP events on the launch stream.  APPNP_SPLIT=0 in the environment gathers whole rows.
+with HIP events on the launch stream.  APPNP_TUNING=1 APPNP_SPLIT=0 in the environment gathers
+whole rows.
 
     python tools/bwd_time.py [--workload products-synth] [--reps 5]
 """

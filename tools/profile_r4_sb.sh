@@ -1,4 +1,5 @@
 #!/bin/bash
+export APPNP_TUNING=1  # round 6: the library reads tuning overrides only with APPNP_TUNING=1
 # Round 4: source-block size of the W16 / W8 passes now that they take a barrier every S blocks
 # (APPNP_SB_ROWS rows per block, APPNP_REM_SYNC_W16 / _W8 = S).  gpurun_out/sb/.
 set -u

@@ -1,4 +1,5 @@
 #!/bin/bash
+export APPNP_TUNING=1  # round 6: the library reads tuning overrides only with APPNP_TUNING=1
 # Round 4: the remainder pass walking its source blocks in step (SYNC, a workgroup barrier
 # per block; APPNP_REM_SYNC = mask of bit LPE: 2 W4, 4 W8, 16 W16) against the free-running
 # waves, for the W16 pass of the 8-rank column slab, the W8 pass (F = 40 = 32 + 8) and the W4

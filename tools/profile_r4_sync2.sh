@@ -1,4 +1,5 @@
 #!/bin/bash
+export APPNP_TUNING=1  # round 6: the library reads tuning overrides only with APPNP_TUNING=1
 # Round 4: the period S of the remainder pass's workgroup barrier (APPNP_REM_SYNC_W<w>=S: every S
 # source blocks), per width, after tools/profile_r4_window.sh found S = 16 faster than free-running
 # waves on the W16 pass (1.79 against 1.94 ms).  W16 (13-column slab of the 8-rank column layout),

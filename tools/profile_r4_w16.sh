@@ -1,4 +1,5 @@
 #!/bin/bash
+export APPNP_TUNING=1  # round 6: the library reads tuning overrides only with APPNP_TUNING=1
 # Round 4: the W16 remainder pass the 8-rank column layout runs on its 13-column
 # products-synth slab (bench.py --layout col --emulate 8:0).  Kernel stats of the shipped pass,
 # of source blocks of 2^13 / 2^14 / 2^16 rows (APPNP_SB_ROWS) and of 1 / 4 / 8 chunks in flight

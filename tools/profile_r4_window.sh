@@ -1,4 +1,5 @@
 #!/bin/bash
+export APPNP_TUNING=1  # round 6: the library reads tuning overrides only with APPNP_TUNING=1
 # Round 4: pacing the remainder pass's waves inside their workgroup.  APPNP_REM_WINDOW_W<w>=D: a
 # wave more than D source blocks ahead of its workgroup's slowest wave sleeps until it catches
 # up (no barrier); APPNP_REM_SYNC_W<w>=S: a workgroup barrier every S blocks.  The W16 pass of

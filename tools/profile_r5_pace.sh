@@ -1,4 +1,5 @@
 #!/bin/bash
+export APPNP_TUNING=1  # round 6: the library reads tuning overrides only with APPNP_TUNING=1
 # Round 5: XCD-wide pacing of the W16 remainder pass on the 8-rank column slab
 # (bench.py --layout col --emulate 8:0: 13 of products-synth's 100 columns, 4 row passes) and of
 # the W8 pass (F = 40 = 32 + 8).  APPNP_REM_PACE_W<w>=p: at every barrier (every 32 blocks) a

@@ -1,4 +1,5 @@
 #!/bin/bash
+export APPNP_TUNING=1  # round 6: the library reads tuning overrides only with APPNP_TUNING=1
 # Round 5: entries in flight per sub-group of the main SpMM (APPNP_UW), read from
 # roofline.kernel_ms (main = the SpMM launches of one untimed propagation).
 set -u

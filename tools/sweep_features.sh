@@ -1,4 +1,5 @@
 #!/bin/bash
+export APPNP_TUNING=1  # round 6: the library reads tuning overrides only with APPNP_TUNING=1
 # Per-iteration time of products-synth against the feature width F (lines per gathered row).
 # Usage: tools/sweep_features.sh [F ...]   (environment passed through, e.g. APPNP_SPLIT=0)
 for f in ${@:-32 64 96 100 128}; do

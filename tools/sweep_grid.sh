@@ -1,4 +1,5 @@
 #!/bin/bash
+export APPNP_TUNING=1  # round 6: the library reads tuning overrides only with APPNP_TUNING=1
 # Grid-cap sweep (APPNP_MAX_BLOCKS: the SpMM grid-strides over rows when capped) on products-synth
 # and arxiv-synth; one bench line per setting into gpurun_out/grid/.
 set -u

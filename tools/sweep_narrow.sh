@@ -1,4 +1,5 @@
 #!/bin/bash
+export APPNP_TUNING=1  # round 6: the library reads tuning overrides only with APPNP_TUNING=1
 # narrow (G-lane group per row) vs wide (wavefront per row) kernels on the per-rank slabs of
 # column layouts (emulated ranks): APPNP_WIDE_ALL=1 forces the wide kernel
 B="python bench.py --steps 5 --warmup 2 --cpu-iters 0"

@@ -1,4 +1,5 @@
 #!/bin/bash
+export APPNP_TUNING=1  # round 6: the library reads tuning overrides only with APPNP_TUNING=1
 # Cache policy of the SpMM streams (StepArgs::nt, APPNP_NT bit mask: 1 col/val, 2 H, 4 Zout
 # non-temporal) on the bench workloads.  Usage: tools/sweep_nt.sh [workload[:dtype]] ...
 B="python bench.py --steps 5 --warmup 2 --cpu-iters 0"

@@ -1,4 +1,5 @@
 B="python bench.py --steps 5 --warmup 2 --cpu-iters 0"
+export APPNP_TUNING=1  # round 6: the library reads tuning overrides only with APPNP_TUNING=1
 tools/gpu_session.sh \
  "sb16k::120::APPNP_SB_ROWS=16384 $B" \
  "sb32k::120::APPNP_SB_ROWS=32768 $B" \

@@ -1,4 +1,5 @@
 #!/bin/bash
+export APPNP_TUNING=1  # round 6: the library reads tuning overrides only with APPNP_TUNING=1
 # Split rows (appnp_blocks.hip) on products-synth: per-iteration time with the path off
 # (APPNP_SPLIT=0) and with the remainder pass's source block size (APPNP_SB_ROWS source rows
 # per block) varied.

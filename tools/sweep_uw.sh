@@ -1,4 +1,5 @@
 #!/bin/bash
+export APPNP_TUNING=1  # round 6: the library reads tuning overrides only with APPNP_TUNING=1
 # Latency-regime shape overrides on the small workloads: entries in flight per sub-group of
 # the wide kernel (APPNP_UW), wide/narrow (APPNP_WIDE), elements per lane (APPNP_VEC).
 # Usage: tools/sweep_uw.sh "workload|ENV=.. ENV=..|..." ...

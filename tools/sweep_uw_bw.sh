@@ -1,4 +1,5 @@
 #!/bin/bash
+export APPNP_TUNING=1  # round 6: the library reads tuning overrides only with APPNP_TUNING=1
 # Entries in flight per sub-group of the wide kernel (APPNP_UW) in the bandwidth regime.
 # Usage: tools/sweep_uw_bw.sh "workload[:F[:dtype]]" ...
 for spec in "${@:-products-synth arxiv-synth}"; do

@@ -1,4 +1,5 @@
 #!/bin/bash
+export APPNP_TUNING=1  # round 6: the library reads tuning overrides only with APPNP_TUNING=1
 # Wide remainder pass (APPNP_GRAPH_SB_W8/_W16) against whole-row gathers (APPNP_SPLIT=0) on the
 # shapes it targets; one bench line per case into gpurun_out/wide/.
 set -u

@@ -1,4 +1,5 @@
 #!/bin/bash
+export APPNP_TUNING=1  # round 6: the library reads tuning overrides only with APPNP_TUNING=1
 # grid-size sweep of the SpMM launch on products-synth (APPNP_MAX_BLOCKS)
 for b in 1024 2048 4096 8192 32768 1000000; do
   echo "max_blocks=$b"
