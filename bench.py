@@ -72,11 +72,11 @@ XGMI_IN_GBS = 7 * 76.8
 #   * requests: one L2 request per nonzero (an entry's 16 LPE bytes lie in one line) at the rate
 #     of the W4 pass with every gather forced to an L2-resident row: 0.665 ms for products-synth's
 #     126,165,965 nonzeros, entry stream included = 189.7 G requests/s.
-# Row passes and direct rows: rem_row_layout, as graph_build_source_blocks has them.
+# Row passes: ceil(rows / (CUs x 16 waves x 640 / LPE rows)), as graph_build_source_blocks has it.
 REM_L2_REQ_RATE = 126_165_965 / 0.665e-3 / 1e9
 REM_L2_REQ_SOURCE = ("DESIGN.md 4.2: the W4 pass with every gather an L2 hit, 0.665 ms for "
                      "126.2 M nonzeros")
-XCDS, CUS, REM_WAVES, REM_LDS_BYTES = 8, 256, 16, 160 * 1024
+XCDS, CUS, REM_WAVES, REM_ROWS_LPE1 = 8, 256, 16, 640
 # N > 1: the whole run's wall budget, below the driver's 600 s bench timeout with
 # room for the launcher, the first `import torch` of a fresh box and the teardown; a candidate
 # is not started with less than MIN_CANDIDATE_S of it left
@@ -314,15 +314,11 @@ def kernel_plan(F_local, K, remainder_cols, sb):
         return ("k_step (one fused SpMM launch per iteration)", "k_step", F_local, 0, 1)
     fs = F_local - r
     lpe = sb["width"] // 4
-    cols = sb.get("cols", sb["width"])
-    rem = (f"k_rem_persist<W{sb['width']}{',vf' if sb['value_free'] else ''}"
-           f"{f',c{cols}' if cols < sb['width'] else ''}>")
+    rem = f"k_rem_persist<W{sb['width']}{',vf' if sb['value_free'] else ''}>"
     if not fs:
-        direct = sb.get("direct_rows", 0)
         return (f"{rem} on all {F_local} columns (narrow rows: one persistent L2-blocked launch "
-                f"per iteration, {sb['row_passes']} row passes"
-                + (f", {direct} rows gathered directly" if direct else "") + ")",
-                f"{rem}[0,{F_local})", 0, r, lpe)
+                f"per iteration, {sb['row_passes']} row passes)", f"{rem}[0,{F_local})", 0, r,
+                lpe)
     return (f"k_step on columns [0, {fs}) + {rem} on the remainder columns [{fs}, {F_local}) "
             "(one persistent L2-blocked launch) per iteration; times are per iteration",
             f"k_step[0,{fs})+{rem}[{fs},{F_local})", fs, r, lpe)
@@ -344,44 +340,24 @@ def rank_traffic_key(workload, dtype_name, runner, K) -> str:
                        bool(getattr(runner, "pipeline", False)))
 
 
-def rem_row_layout(rows, lpe, cols=None):
-    """(row passes, rows per wave group, direct rows) of the W = 4 lpe remainder pass sized for
-    ``cols`` columns, as graph_build_source_blocks lays it out: a row's sums take 16 B (LPE = 1)
-    or 4 cols B of LDS, 16 waves x 256 CUs hold 160 KiB / (16 x that) rows each per row pass,
-    and when the last pass would hold at most 1/8 of the rows it is dropped and those rows are
-    gathered directly."""
-    cols = 4 * lpe if lpe == 1 or not cols else cols
-    row_bytes = 16 if lpe == 1 else 4 * cols
-    max_rg = REM_LDS_BYTES // (REM_WAVES * row_bytes)
-    cap = CUS * REM_WAVES * max_rg
-    passes = max(1, -(-rows // cap))
-    if passes > 1 and rows - (passes - 1) * cap <= rows // 8:
-        return passes - 1, max_rg, rows - (passes - 1) * cap
-    return passes, max(1, -(-rows // (passes * CUS * REM_WAVES))), 0
-
-
-def remainder_floor(n, rows, nnz, lpe, cols=None):
+def remainder_floor(n, rows, nnz, lpe):
     """The W = 4 lpe remainder pass's floor from counts (see REM_L2_REQ_RATE): the larger of its
-    compulsory L2 fill (+ entry stream, + one line request per nonzero of its direct rows) from
-    beyond L2 and its L2 requests at the all-hit rate."""
-    passes, _, direct = rem_row_layout(rows, lpe, cols)
+    compulsory L2 fill (+ entry stream) from beyond L2 and its L2 requests at the all-hit rate."""
+    slot_rows = CUS * REM_WAVES * (REM_ROWS_LPE1 // lpe)
+    passes = max(1, -(-rows // slot_rows))
     fill_lines = passes * XCDS * n * 16 * lpe / 128
-    direct_lines = nnz * direct / rows if rows else 0.0
     entry_bytes = 4 * nnz
-    fill_ms = ((fill_lines + direct_lines) / (GATHER_LINE_CEILING * 1e9)
-               + entry_bytes / (HBM_PEAK_GBS * 1e9)) * 1e3
+    fill_ms = (fill_lines / (GATHER_LINE_CEILING * 1e9) + entry_bytes / (HBM_PEAK_GBS * 1e9)) * 1e3
     req_ms = nnz / (REM_L2_REQ_RATE * 1e9) * 1e3
     return {"ms": max(fill_ms, req_ms), "fill_ms": fill_ms, "l2_request_ms": req_ms,
-            "row_passes": passes, "fill_lines": fill_lines, "direct_rows": direct,
-            "direct_lines": direct_lines,
+            "row_passes": passes, "fill_lines": fill_lines,
             "kind": "count floor (not a measured rate): max(row passes x 8 XCDs x table / 128-B "
-                    f"lines + one line per nonzero of the direct rows at {GATHER_LINE_CEILING} "
-                    "G lines/s + 4 B/entry at the HBM peak, one L2 request per nonzero at "
-                    f"{REM_L2_REQ_RATE:.1f} G/s ({REM_L2_REQ_SOURCE}))"}
+                    f"lines at {GATHER_LINE_CEILING} G lines/s + 4 B/entry at the HBM peak, "
+                    f"one L2 request per nonzero at {REM_L2_REQ_RATE:.1f} G/s ({REM_L2_REQ_SOURCE}))"}
 
 
 def roofline(*, n, rows, nnz, F_local, esz, avg_iter_ms, fs, r, lpe, exchange_in_bytes=0,
-             kernel="", kernel_key="", traffic=None, cols=None):
+             kernel="", kernel_key="", traffic=None):
     """The roofline block of one rank.
 
     achieved = B_iter / iteration time with B_iter = 4(rows+1) + 8 nnz + (n + 2 rows) F s: the
@@ -415,7 +391,7 @@ def roofline(*, n, rows, nnz, F_local, esz, avg_iter_ms, fs, r, lpe, exchange_in
         dense = 2 * rows * ld * s
     lines = nnz * lpn + (stream + dense) / 128
     width = 4 * lpe
-    rem = remainder_floor(n, rows, nnz, lpe, cols) if r else None
+    rem = remainder_floor(n, rows, nnz, lpe) if r else None
     rem_ms = rem["ms"] if r else 0.0
     compute_ms = lines / (GATHER_LINE_CEILING * 1e9) * 1e3 + rem_ms
     exchange_ms = exchange_in_bytes / (XGMI_IN_GBS * 1e9) * 1e3
@@ -867,7 +843,7 @@ def main(argv=None):
         rl = roofline(n=n, rows=graph.rows, nnz=graph.nnz_hat, F_local=F_local, esz=esz,
                       avg_iter_ms=avg_iter_ms, fs=fs, r=r, lpe=lpe,
                       exchange_in_bytes=exchange_in, kernel=desc, kernel_key=kkey,
-                      traffic=committed_traffic(tkey), cols=sb.get("cols") if sb else None)
+                      traffic=committed_traffic(tkey))
         rl["source_blocks"] = sb
         rl["traffic_key"] = tkey
         rl["kernel_ms"] = kernel_split(runner.run, dev, K, avg_iter_ms)

@@ -42,9 +42,10 @@ extern "C" {
 #endif
 
 /* 2 (round 6): appnp_dist_workspace_bytes reserves staging for a misaligned H / Z (a larger
- * workspace than version 1 asked for); APPNP_GRAPH_SB_COLS; appnp_graph_source_block_rows;
- * the per-launch timer brackets each launch (start and end events) and has the kinds
- * APPNP_KT_LOCAL / _REMOTE / _XCHG; appnp_tuning_overrides / appnp_tuning_names. */
+ * workspace than version 1 asked for); the pipelined row steps (appnp_graph_shard_offsets,
+ * appnp_step_shards, appnp_step_split_shards, appnp_dist_set_broadcast); the per-launch timer
+ * brackets each launch (start and end events) and has the kinds APPNP_KT_LOCAL / _REMOTE /
+ * _XCHG; appnp_tuning_overrides / appnp_tuning_names. */
 #define PPNP_AMD_ABI_VERSION 2
 
 typedef struct appnp_graph appnp_graph;
@@ -87,17 +88,6 @@ enum appnp_norm { APPNP_NORM_SYM = 0, APPNP_NORM_RW = 1 };
  * launch.  Same memory as APPNP_GRAPH_SOURCE_BLOCKS (segments padded to 32 / 16 entries). */
 #define APPNP_GRAPH_SB_W8 0x400
 #define APPNP_GRAPH_SB_W16 0x800
-
-/* OR into `mode` with APPNP_GRAPH_SB_W8 / _W16: size the remainder pass for c remainder columns
- * (1 <= c <= the copy's width; 0 or absent: the whole width).  The pass keeps each row's sums
- * in LDS, 4 c bytes instead of 16 or 32 / 64, so a row pass holds more rows: the 13-column
- * slabs of F = 100 over 8 column ranks take 3 row passes instead of 4 on products-synth (the
- * rows the last pass would hold, when they are at most 1/8 of them, are gathered directly from
- * the CSR instead; appnp_graph_source_block_rows).  Propagations whose remainder is wider than
- * c gather whole rows.  Ignored for APPNP_GRAPH_SOURCE_BLOCKS (always 4). */
-#define APPNP_GRAPH_SB_COLS_SHIFT 16
-#define APPNP_GRAPH_SB_COLS_MASK (0x1f << APPNP_GRAPH_SB_COLS_SHIFT)
-#define APPNP_GRAPH_SB_COLS(c) (((c) & 0x1f) << APPNP_GRAPH_SB_COLS_SHIFT)
 
 /* storage type of H / Z (accumulation is always fp32) */
 enum appnp_dtype { APPNP_F32 = 0, APPNP_BF16 = 1 };
@@ -225,12 +215,6 @@ int appnp_propagate_remainder_cols(const appnp_graph* g, int64_t f, int dtype, i
  * remainder-pass launches enqueued on this graph so far (which path a propagation took). */
 int appnp_graph_source_block_layout(const appnp_graph* g, int* width, int64_t* entries,
                                     int* value_free, int* row_passes, int64_t* launches);
-
-/* The same copy's row layout: *cols remainder columns its pass holds sums for
- * (APPNP_GRAPH_SB_COLS; 0 = not built), *rows_per_group rows of one wave's group, and
- * *direct_rows held rows in no group, gathered straight from the CSR by the pass. */
-int appnp_graph_source_block_rows(const appnp_graph* g, int* cols, int* rows_per_group,
-                                  int64_t* direct_rows);
 
 /*
  * Z = APPNP_K(H):  Z_0 = H;  Z_{k+1} = (1-alpha) (M_k o A_hat) Z_k + alpha H,  k < K.

@@ -33,12 +33,6 @@ GRAPH_SOURCE_BLOCKS = 0x200
 GRAPH_SB_W8 = 0x400  # remainder of up to 8 columns (include/ppnp_amd.h)
 GRAPH_SB_W16 = 0x800  # up to 16
 
-
-def GRAPH_SB_COLS(c: int) -> int:
-    """APPNP_GRAPH_SB_COLS(c): size the W8 / W16 remainder pass for c columns."""
-    return (int(c) & 0x1F) << 16
-
-
 F32, BF16 = 0, 1
 PART_ALL, PART_LOCAL, PART_REMOTE = 0, 1, 2
 SHARDS_FIRST, SHARDS_ACC, SHARDS_LAST, SHARDS_ONLY = 0, 1, 2, 3  # appnp_shard_mode
@@ -117,8 +111,6 @@ _SIGS = {
     "appnp_kernel_timer_end": (_i32, [_vp, _vp, _i32, C.POINTER(_i32)]),
     "appnp_tuning_overrides": (C.c_char_p, []),
     "appnp_tuning_names": (C.c_char_p, []),
-    "appnp_graph_source_block_rows": (_i32, [_vp, C.POINTER(_i32), C.POINTER(_i32),
-                                             C.POINTER(_i64)]),
     "appnp_step": (
         _i32,
         [_vp, _i32, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _f32,

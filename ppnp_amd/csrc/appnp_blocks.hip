@@ -61,15 +61,12 @@
 // F = 40 = 32 + 8 3.68 against 4.44 ms (profiles/r2_wide_remainder.txt).
 // LPE = 1 is the pass above, unchanged.
 //
-// Packed accumulators and direct rows (W8 / W16 copies sized for c remainder columns,
-// APPNP_GRAPH_SB_COLS).  A row's sums take 4 c bytes of LDS, not 16 LPE: pf = c / 4 whole 16-B
-// pieces, then pc = c % 4 floats of the next piece -- 52 B for the 13-column slabs of F = 100 on
-// 8 column ranks instead of 64, so a wave group holds 196 rows instead of 160.  When the rows
-// that do not fit the last row pass are few (<= 1/8 of the rows: 40,581 of products-synth's
-// 2,449,029 at 13 columns), that pass is dropped and those rows -- [direct_lo, rows), in no row
-// group -- are gathered straight from the CSR, one wave per row, before the sweep: one line
-// request per nonzero of 1.7 % of the rows instead of a 4th refill of the 157 MB table on every
-// XCD.
+// The sums of a wave group live in LDS piece-major: piece q of row r at slot q rg + r.  The tails
+// of one piece in an 8-lane group of a 16-B LDS access are then consecutive slots for
+// consecutive rows; row-major (a 64-B row stride on a W16 copy) put every row of one parity in
+// the same 4 banks: 2.2e8 bank-conflict cycles per launch of the 8-rank column slab's pass
+// (SQ_LDS_BANK_CONFLICT), 5.2e7 piece-major; W16 1.825 -> 1.817 ms, W8 0.977 -> 0.970 ms
+// (profiles/r6_w16_ab.txt).
 #include <algorithm>
 #include <cstdlib>
 
@@ -113,17 +110,7 @@ struct RemLayout {
   int32_t nb, br_log2, slots, rg, passes;
   int32_t scale_out;    // VF: the output is the next remainder buffer (store dr o y)
   int32_t sync;         // > 0: workgroup barrier after every `sync` source blocks (k_rem_persist)
-  int32_t pf, pc;       // a row's sums in LDS: pf whole 16-B pieces, then pc (< 4) floats of
-                        // piece pf (LPE = 1: pf = 1, pc = 0)
-  int64_t direct_lo;    // held rows [direct_lo, n_rows) are in no row group: gathered directly
 };
-
-// Bytes of LDS one row's sums take (see RemLayout::pf / pc), and one wave's slice of rg rows
-// (16-B aligned, so every wave's pieces are)
-__host__ __device__ constexpr int rem_row_bytes(int pf, int pc) { return 16 * pf + 4 * pc; }
-__host__ __device__ constexpr int64_t rem_slice_bytes(int64_t rg, int pf, int pc) {
-  return (rg * rem_row_bytes(pf, pc) + 15) / 16 * 16;
-}
 
 // ---- segmented inclusive scan over the 64 lanes (rows non-decreasing across lanes) --------
 // DPP (gfx9 family): row_shr:n shifts within each 16-lane row; row_bcast:15 / row_bcast:31
@@ -276,58 +263,21 @@ __device__ __forceinline__ void rem_finish_piece(const StepArgs& a, const RemLay
   }
 }
 
-// The wave's LDS sums of a row group, piece-major: piece q of row `row` is accA[q * rg + row]
-// for q < pf, float c < pc of piece pf is accB[c * rg + row]; the rest of a row is never stored
-// (its columns lie past the remainder the copy was sized for, and gather zeros).  LPE = 1: accA
-// only.  Piece-major, the tails of one piece in a lane group (8 lanes of a 16-B access) hit
-// consecutive 16-B slots for consecutive rows; row-major (a 64-B row stride on a W16 copy) put
-// every row of one parity in the same 4 banks -- 4-way conflicts, 2.2e8 extra LDS cycles per
-// launch of the 13-column slab's pass (SQ_LDS_BANK_CONFLICT, profiles/r6_w16_sq.txt).
+// The wave's LDS sums of a row group, piece-major (see the file comment): piece q of row `row`
+// is acc[q * rg + row].
 #ifdef APPNP_REM_ROW_MAJOR  // measurement variant: the round-5 row-major sums
-#define REM_SLOT(q, row) ((row) * L.pf + (q))
+#define REM_SLOT(q, row) ((row) * LPE + (q))
 #else
 #define REM_SLOT(q, row) ((q) * L.rg + (row))
 #endif
-template <int LPE>
-__device__ __forceinline__ void acc_add(f32x4* accA, float* accB, const RemLayout& L, int row,
-                                        int q, const f32x4& v) {
-  if (LPE == 1 || q < L.pf) {
-    f32x4& s = accA[LPE == 1 ? row : REM_SLOT(q, row)];
-    s = f32x4{s.x + v.x, s.y + v.y, s.z + v.z, s.w + v.w};
-  } else if (q == L.pf && L.pc > 0) {
-    // LDS float adds without a return (ds_add_f32): no read to wait for on this short path.
-    // Not for atomicity -- a (row, piece) has one tail per chunk, and the wave that owns the
-    // row adds its chunks in order, so the sums stay deterministic
-    float* b = accB + row;
-    __hip_atomic_fetch_add(b, v.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-    if (L.pc > 1)
-      __hip_atomic_fetch_add(b + L.rg, v.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-    if (L.pc > 2)
-      __hip_atomic_fetch_add(b + 2 * L.rg, v.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-  }
-}
-
-template <int LPE>
-__device__ __forceinline__ f32x4 acc_get(const f32x4* accA, const float* accB, const RemLayout& L,
-                                         int row, int q) {
-  if (LPE == 1 || q < L.pf) return accA[LPE == 1 ? row : REM_SLOT(q, row)];
-  f32x4 v = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-  if (q == L.pf && L.pc > 0) {
-    const float* b = accB + row;
-    v.x = b[0];
-    if (L.pc > 1) v.y = b[L.rg];
-    if (L.pc > 2) v.z = b[2 * L.rg];
-  }
-  return v;
-}
 
 // Chunks [c_begin, c_end) of a wave's entry stream: gather, weight, segmented scan, and the
 // run tails' adds into the wave's LDS rows.  U chunks in flight; the source block of chunk c is
 // cblk[c].
 template <int U, bool VF, int LPE>
 __device__ __forceinline__ void rem_walk(const StepArgs& a, const RemLayout& L,
-                                         const f32x4* __restrict__ z, f32x4* accA, float* accB,
-                                         int64_t r0, int32_t c_begin, int32_t c_end) {
+                                         const f32x4* __restrict__ z, f32x4* acc, int64_t r0,
+                                         int32_t c_begin, int32_t c_end) {
   constexpr int CH = kWave / LPE;  // entries per chunk; piece q of entry e on lane q * CH + e
   const int lane = threadIdx.x & (kWave - 1);
   const int q = lane / CH, le = lane % CH;
@@ -400,7 +350,10 @@ __device__ __forceinline__ void rem_walk(const StepArgs& a, const RemLayout& L,
       const unsigned long long heads = __ballot(lane == 0 || prev != key || !act);
       seg_scan<CH>(key, v, heads);
       const bool tail = le == CH - 1 || ((heads >> (lane + 1)) & 1ull);
-      if (act && tail) acc_add<LPE>(accA, accB, L, row, q, v);
+      if (act && tail) {
+        f32x4& t = acc[REM_SLOT(q, row)];
+        t = f32x4{t.x + v.x, t.y + v.y, t.z + v.z, t.w + v.w};
+      }
     }
 #ifdef APPNP_REM_PREFETCH
 #pragma unroll
@@ -410,62 +363,6 @@ __device__ __forceinline__ void rem_walk(const StepArgs& a, const RemLayout& L,
       wt[u] = wtn[u];
     }
 #endif
-  }
-}
-
-// The direct rows [L.direct_lo, n_rows): one wave per row, straight from the held rows' CSR
-// (a.row_ptr / a.col / a.val), CH = 64 / LPE entries per round and U rounds in flight, lane
-// q * CH + e gathering piece q of entry e.  A value-free (unit) layout ignores a.val: its
-// buffers hold dr o Z_rem, as the blocked entries assume.  The CH lanes of a piece are summed by
-// a fixed butterfly, and the row finishes through the same epilogue as a row group's.
-template <int EPI, int U, bool VF, int LPE>
-__device__ __forceinline__ void rem_direct(const StepArgs& a, const RemLayout& L,
-                                           const f32x4* __restrict__ z, int64_t slot) {
-  constexpr int CH = kWave / LPE;
-  const int lane = threadIdx.x & (kWave - 1);
-  const int q = lane / CH, le = lane % CH;
-  const bool piece_on = LPE == 1 || 4 * q < a.f;  // a piece past the valid columns gathers 0
-  const int64_t stride = (int64_t)gridDim.x * kRemWaves;
-  for (int64_t i = L.direct_lo + slot; i < a.n_rows; i += stride) {
-    const int32_t beg = a.row_ptr[i], end = a.row_ptr[i + 1];
-    f32x4 acc = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    for (int32_t e0 = beg; e0 < end; e0 += U * CH) {
-      int32_t c[U];
-      float w[U];
-      bool act[U];
-      f32x4 zv[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int32_t e = e0 + u * CH + le;
-        act[u] = e < end;
-        c[u] = act[u] ? ld_nt<int32_t>(a.col + e) : 0;
-        w[u] = act[u] ? ((VF || !a.val) ? 1.0f : ld_nt<float>(a.val + e)) : 0.0f;
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        zv[u] = (act[u] && piece_on) ? z[LPE == 1 ? (int64_t)c[u] : (int64_t)c[u] * LPE + q]
-                                     : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const float ww = act[u] && a.drop_on ? edge_weight(w[u], a.row_lo + i, c[u], a) : w[u];
-        acc = f32x4{fmaf(ww, zv[u].x, acc.x), fmaf(ww, zv[u].y, acc.y),
-                    fmaf(ww, zv[u].z, acc.z), fmaf(ww, zv[u].w, acc.w)};
-      }
-    }
-#pragma unroll
-    for (int o = 1; o < CH; o <<= 1) {
-      acc.x += __shfl_xor(acc.x, o);
-      acc.y += __shfl_xor(acc.y, o);
-      acc.z += __shfl_xor(acc.z, o);
-      acc.w += __shfl_xor(acc.w, o);
-    }
-    if (le == 0) {
-      if constexpr (LPE == 1)
-        rem_finish<EPI, VF>(a, L, i, acc);
-      else
-        rem_finish_piece<EPI, VF, LPE>(a, L, i, q, acc);
-    }
   }
 }
 
@@ -490,42 +387,34 @@ __global__ __launch_bounds__(kRemThreads) void k_rem_persist(StepArgs a, RemLayo
   extern __shared__ f32x4 rem_acc[];
   const int lane = threadIdx.x & (kWave - 1);
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  // this wave's slice of LDS: rg rows of pf pieces, then rg rows of pc floats
-  char* base = reinterpret_cast<char*>(rem_acc) + wv * rem_slice_bytes(L.rg, L.pf, L.pc);
-  f32x4* accA = reinterpret_cast<f32x4*>(base);
-  float* accB = reinterpret_cast<float*>(base + (int64_t)L.rg * L.pf * 16);
+  f32x4* acc = rem_acc + (int64_t)wv * L.rg * LPE;  // this wave's rg rows x LPE pieces
   const f32x4* __restrict__ z = static_cast<const f32x4*>(a.zin);
   const int64_t slot = (int64_t)blockIdx.x * kRemWaves + wv;
-  // the rows no row group holds, before the sweep: no barrier inside, so every wave still
-  // reaches the sweep's barriers
-  if (L.direct_lo < a.n_rows) rem_direct<EPI, 4, VF, LPE>(a, L, z, slot);
-  const int64_t held = min<int64_t>(a.n_rows, L.direct_lo);  // rows of the row groups
   for (int p = 0; p < L.passes; ++p) {
     const int64_t g = (int64_t)p * L.slots + slot;
     const int64_t r0 = g * L.rg;
-    const int rows = (int)max<int64_t>(0, min<int64_t>(L.rg, held - r0));
-    for (int r = lane; r < L.rg * L.pf; r += kWave) accA[r] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    for (int r = lane; r < L.rg * L.pc; r += kWave) accB[r] = 0.0f;
+    const int rows = (int)max<int64_t>(0, min<int64_t>(L.rg, a.n_rows - r0));
+    for (int r = lane; r < L.rg * LPE; r += kWave) acc[r] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     if (L.sync > 0) {
       // every wave runs the same nb blocks (an empty segment is 0 chunks) in the same steps,
       // so every wave reaches every barrier; a wave's segments are contiguous in its stream
       for (int b = 0; b < L.nb; b += L.sync) {
-        rem_walk<U, VF, LPE>(a, L, z, accA, accB, r0, L.off[g * L.nb + b] / CH,
+        rem_walk<U, VF, LPE>(a, L, z, acc, r0, L.off[g * L.nb + b] / CH,
                              L.off[g * L.nb + min(b + L.sync, L.nb)] / CH);
         __syncthreads();
       }
     } else {
       // this wave's stream: blocks 0..nb-1 back to back, each a whole number of chunks
-      rem_walk<U, VF, LPE>(a, L, z, accA, accB, r0, L.off[g * L.nb] / CH,
-                           L.off[(g + 1) * L.nb] / CH);
+      rem_walk<U, VF, LPE>(a, L, z, acc, r0, L.off[g * L.nb] / CH, L.off[(g + 1) * L.nb] / CH);
     }
     if constexpr (LPE == 1) {
-      for (int r = lane; r < rows; r += kWave) rem_finish<EPI, VF>(a, L, r0 + r, accA[r]);
+      for (int r = lane; r < rows; r += kWave) rem_finish<EPI, VF>(a, L, r0 + r, acc[r]);
     } else {
-      // row-major over (row, piece), so a wave's stores cover whole rows of the output
+      // row-major over (row, piece), so a wave's stores cover whole rows of the output (a
+      // piece-major order here, 16-B stores 16 LPE B apart, measured 5 % slower at W16)
       for (int r = lane; r < rows * LPE; r += kWave)
         rem_finish_piece<EPI, VF, LPE>(a, L, r0 + r / LPE, r % LPE,
-                                       acc_get<LPE>(accA, accB, L, r / LPE, r % LPE));
+                                       acc[REM_SLOT(r % LPE, r / LPE)]);
     }
   }
 }
@@ -722,24 +611,15 @@ int test_env(const char* name, int dflt) {
 
 // The regrouped copy of A_hat for the persistent remainder pass.  Best-effort at the caller
 // (appnp_graph_create_rows): APPNP_ENOTSUP / APPNP_ERANGE / APPNP_ENOMEM leave the graph
-// without it, and appnp_propagate gathers whole rows.  cols: the remainder columns the pass is
-// sized for (1 .. 4 lpe; LPE = 1 always 4): a row's sums take 4 cols bytes of LDS.
-int graph_build_source_blocks(appnp_graph* g, int lpe, int cols, const int32_t* a_indptr,
+// without it, and appnp_propagate gathers whole rows.
+int graph_build_source_blocks(appnp_graph* g, int lpe, const int32_t* a_indptr,
                               const int32_t* a_indices, int64_t a_nnz, hipStream_t s) {
   // the held rows [row_lo, row_hi) in row groups; source blocks over all n global columns
   const int64_t rows = g->row_hi - g->row_lo;
   const bool partial = g->row_lo != 0 || rows != g->n;
   if (lpe != 1 && lpe != 2 && lpe != 4) return APPNP_EINVAL;
-  if (lpe == 1 || cols <= 0) cols = 4 * lpe;
-  if (cols > 4 * lpe) return APPNP_EINVAL;
-  // APPNP_SB_COLS (tuning override): size the pass for more columns than requested (A/B of the
-  // packed sums); never fewer, which would drop the requested ones
-  if (lpe > 1) cols = std::min(4 * lpe, std::max(cols, tuning_env("APPNP_SB_COLS", 0)));
-  const int pf = cols / 4, pc = cols % 4;  // RemLayout::pf / pc
   const int chunk = kRemChunk / lpe;     // entries per chunk (one per lpe lanes)
-  // rows per wave group: 16 waves x max_rg rows x 4 cols bytes of LDS
-  const int max_rg = kRemLdsBytes / (kRemWaves * rem_row_bytes(pf, pc));
-  if (max_rg >= (1 << kRemRowBits)) return APPNP_EINVAL;
+  const int max_rg = kRemMaxRg / lpe;    // rows per wave group: 16 x max_rg x 16 lpe B of LDS
   // APPNP_SB_ROWS: tuning override of the block size (a power of two, 2^10..2^20 rows)
   static const int br_log2 = [] {
     const int x = tuning_env("APPNP_SB_ROWS", 1 << kSourceBlockLog2);
@@ -763,21 +643,8 @@ int graph_build_source_blocks(appnp_graph* g, int lpe, int cols, const int32_t* 
       cus <= 0)
     return APPNP_EDEVICE;
   const int64_t slots = (int64_t)cus * kRemWaves;
-  const int64_t cap = slots * max_rg;  // rows one row pass holds
-  int64_t passes = std::max<int64_t>(1, (rows + cap - 1) / cap);
-  int64_t rg = std::max<int64_t>(1, (rows + passes * slots - 1) / (passes * slots));
-  // direct rows: when the last row pass would hold at most 1/8 of the rows, drop it and gather
-  // those rows straight from the CSR (one line request per nonzero) rather than refill the
-  // whole table on every XCD once more
-  int64_t direct_lo = rows;
-  // APPNP_SB_DIRECT (tuning override): the 1/d share of the rows below which they go direct
-  // (0: never)
-  static const int direct_den = tuning_env("APPNP_SB_DIRECT", 8);
-  if (passes > 1 && direct_den > 0 && rows - (passes - 1) * cap <= rows / direct_den) {
-    passes -= 1;
-    rg = max_rg;
-    direct_lo = passes * cap;
-  }
+  const int64_t passes = std::max<int64_t>(1, (rows + slots * max_rg - 1) / (slots * max_rg));
+  const int64_t rg = std::max<int64_t>(1, (rows + passes * slots - 1) / (passes * slots));
   const int64_t cells = passes * nb * slots;
   if (cells + 1 > INT32_MAX) return APPNP_ERANGE;
   int rc = APPNP_OK;
@@ -793,9 +660,6 @@ int graph_build_source_blocks(appnp_graph* g, int lpe, int cols, const int32_t* 
   // APPNP_REM_VF=0 keeps the values (tuning override)
   const bool vf = g->unit && tuning_env("APPNP_REM_VF", 1) != 0;
   const int64_t n_groups = passes * slots;
-  // the gather-locality measure over the whole A (k_near_all) for a row partition, or when the
-  // walks skip the direct rows; else the walk's own count over the held rows
-  const bool whole_a = partial || direct_lo < rows;
   const unsigned grid = (unsigned)((n_groups + kWalkWaves - 1) / kWalkWaves);
   const size_t lds = (size_t)kWalkWaves * nb * sizeof(int32_t);
   int64_t h_tot[2] = {0, 0};  // padded entries, near entries
@@ -804,12 +668,11 @@ int graph_build_source_blocks(appnp_graph* g, int lpe, int cols, const int32_t* 
       ok(hipMalloc(&bsum, scan_partials(cells) * sizeof(int64_t))) &&
       ok(hipMalloc(&tot, 2 * sizeof(int64_t))) &&
       ok(hipMemsetAsync(tot, 0, 2 * sizeof(int64_t), s))) {
-    // the walks cover the rows of the row groups, [0, direct_lo)
     hipLaunchKernelGGL(k_rb_walk<false>, dim3(grid), dim3(kBlock), lds, s, g->row_ptr, g->col,
-                       g->val, direct_lo, g->row_lo, (int)rg, (int)nb, br_log2, chunk, n_groups,
-                       cnt, nullptr, nullptr, nullptr,
+                       g->val, rows, g->row_lo, (int)rg, (int)nb, br_log2, chunk, n_groups, cnt,
+                       nullptr, nullptr, nullptr,
                        reinterpret_cast<unsigned long long*>(tot + 1));
-    if (whole_a && a_nnz > 0 && ok(hipGetLastError()) &&
+    if (partial && a_nnz > 0 && ok(hipGetLastError()) &&
         ok(hipMemsetAsync(tot + 1, 0, sizeof(int64_t), s))) {
       // the near count of the WHOLE A (replacing the held rows' count of the walk)
       const int64_t nblk = std::min<int64_t>((g->n + kBlock - 1) / kBlock, 4096);
@@ -841,7 +704,7 @@ int graph_build_source_blocks(appnp_graph* g, int lpe, int cols, const int32_t* 
          ok(hipMalloc(&g->rb_dr, std::max<int64_t>(1, g->n) * sizeof(float)))) &&
         ok(hipMalloc(&g->rb_cblk, std::max<int64_t>(1, total / chunk) * sizeof(int32_t)))) {
       hipLaunchKernelGGL(k_rb_walk<true>, dim3(grid), dim3(kBlock), lds, s, g->row_ptr, g->col,
-                         g->val, direct_lo, g->row_lo, (int)rg, (int)nb, br_log2, chunk, n_groups,
+                         g->val, rows, g->row_lo, (int)rg, (int)nb, br_log2, chunk, n_groups,
                          nullptr,
                          g->rb_off,
                          g->rb_ent, g->rb_val, nullptr);
@@ -859,7 +722,7 @@ int graph_build_source_blocks(appnp_graph* g, int lpe, int cols, const int32_t* 
                            dim3(kBlock), 0, s, g->rb_off, cells, (int)nb, chunk, g->rb_cblk);
       // near entries per entry of A_hat: the held rows' (full graph) or the whole graph's
       // (row partition: A's off-diagonal entries + the n diagonal ones)
-      const double denom = whole_a ? (double)(a_nnz + g->n) : (double)g->nnz_hat;
+      const double denom = partial ? (double)(a_nnz + g->n) : (double)g->nnz_hat;
       if (ok(hipGetLastError()) && ok(hipStreamSynchronize(s)))
         g->near_frac = denom > 0 ? (double)h_tot[1] / denom : 0.0;
     }
@@ -893,9 +756,6 @@ int graph_build_source_blocks(appnp_graph* g, int lpe, int cols, const int32_t* 
   g->rb_rg = (int32_t)rg;
   g->rb_passes = (int32_t)passes;
   g->rb_lpe = lpe;
-  g->rb_pf = pf;
-  g->rb_pc = pc;
-  g->rb_direct_lo = direct_lo;
   return APPNP_OK;
 }
 
@@ -925,11 +785,9 @@ hipError_t launch_remainder(const appnp_graph* g, const StepArgs& a_in, int epi,
   const bool vf = g->rb_val == nullptr;
   const int lpe = g->rb_lpe;
   const int sync = rem_sync_blocks(lpe);
-  RemLayout L{g->rb_off,    g->rb_ent,   g->rb_val,   g->rb_cblk,  g->rb_dl,
-              g->rb_dr,     g->rb_nb,    g->rb_br_log2, g->rb_slots, g->rb_rg,
-              g->rb_passes, to_rem ? 1 : 0, sync,     g->rb_pf,    g->rb_pc,
-              g->rb_direct_lo};
-  const size_t lds = (size_t)kRemWaves * rem_slice_bytes(g->rb_rg, g->rb_pf, g->rb_pc);
+  RemLayout L{g->rb_off, g->rb_ent, g->rb_val, g->rb_cblk, g->rb_dl, g->rb_dr, g->rb_nb,
+              g->rb_br_log2, g->rb_slots, g->rb_rg, g->rb_passes, to_rem ? 1 : 0, sync};
+  const size_t lds = (size_t)kRemWaves * g->rb_rg * lpe * sizeof(f32x4);
   const dim3 grid((unsigned)g->rb_grid), block(kRemThreads);
   if (epi == EPI_BWD)
     return vf ? launch_rem_lpe<EPI_BWD, true>(lpe, grid, block, lds, s, a, L)

@@ -78,8 +78,7 @@ void ktimer_mark(hipStream_t s, int kind) {
 const char* const kTuningNames[] = {
     "APPNP_SPLIT",       "APPNP_VEC",         "APPNP_WIDE",         "APPNP_UW",
     "APPNP_UN",          "APPNP_NT",          "APPNP_MAX_BLOCKS",   "APPNP_REM_SYNC_W4",
-    "APPNP_REM_SYNC_W8", "APPNP_REM_SYNC_W16", "APPNP_SB_ROWS",     "APPNP_REM_VF",
-    "APPNP_SB_COLS",     "APPNP_SB_DIRECT"};
+    "APPNP_REM_SYNC_W8", "APPNP_REM_SYNC_W16", "APPNP_SB_ROWS",     "APPNP_REM_VF"};
 
 bool tuning_on() {
   static const bool on = [] {
@@ -197,8 +196,7 @@ int64_t remainder_cols(const appnp_graph* g, int64_t f, int dtype, bool aligned)
   // than the remainder pass (products-local, ~90 % near entries: 4.0 ms whole rows, 3.7 ms for
   // the 3-line main part alone, 8.5 ms split).  Uniform products-synth: 1.3 % near.
   if (g->near_frac > kSplitMaxNear && enabled != 2) return 0;  // APPNP_SPLIT=2: regardless
-  // the pass holds sums for the columns the copy was sized for (APPNP_GRAPH_SB_COLS)
-  const int64_t w = appnp::source_block_cols(g);
+  const int64_t w = 4 * (int64_t)g->rb_lpe;
   const int64_t r = f > 32 ? f % 32 : f;
   if (f <= 32 && f > w) return 0;  // one line per row already, or too wide for the pass
   // beside a main part, a remainder of 9-16 columns costs as much as its extra line
@@ -383,11 +381,8 @@ int appnp_graph_create_rows(const int32_t* indptr, const int32_t* indices, const
   const int sb_lpe = (mode & APPNP_GRAPH_SB_W16) ? 4 : (mode & APPNP_GRAPH_SB_W8) ? 2 : 1;
   const bool want_sb = (mode & (APPNP_GRAPH_SOURCE_BLOCKS | APPNP_GRAPH_SB_W8 |
                                 APPNP_GRAPH_SB_W16)) != 0;
-  // the remainder columns the copy is sized for (0: its whole width 4 sb_lpe)
-  const int sb_cols = (mode & APPNP_GRAPH_SB_COLS_MASK) >> APPNP_GRAPH_SB_COLS_SHIFT;
-  if (sb_cols > 4 * sb_lpe) return APPNP_EINVAL;
   mode &= ~(APPNP_GRAPH_TRANSPOSE | APPNP_GRAPH_SOURCE_BLOCKS | APPNP_GRAPH_SB_W8 |
-            APPNP_GRAPH_SB_W16 | APPNP_GRAPH_SB_COLS_MASK);
+            APPNP_GRAPH_SB_W16);
   if (mode != APPNP_NORM_SYM && mode != APPNP_NORM_RW) return APPNP_EINVAL;
   if (row_lo < 0 || row_hi < row_lo || row_hi > n) return APPNP_EINVAL;
   if (want_t && (row_lo != 0 || row_hi != n)) return APPNP_EINVAL;
@@ -406,8 +401,7 @@ int appnp_graph_create_rows(const int32_t* indptr, const int32_t* indices, const
   // appnp_graph_source_blocks reports whether it was built.
   if (rc == APPNP_OK && want_sb) {
     const int sb =
-        appnp::graph_build_source_blocks(g, sb_lpe, sb_cols, indptr, indices, nnz,
-                                         as_stream(stream));
+        appnp::graph_build_source_blocks(g, sb_lpe, indptr, indices, nnz, as_stream(stream));
     if (sb != APPNP_OK && sb != APPNP_ENOTSUP && sb != APPNP_ERANGE && sb != APPNP_ENOMEM)
       rc = sb;
   }
@@ -511,16 +505,6 @@ int appnp_graph_source_block_layout(const appnp_graph* g, int* width, int64_t* e
   if (value_free) *value_free = built && g->rb_val == nullptr ? 1 : 0;
   if (row_passes) *row_passes = built ? g->rb_passes : 0;
   if (launches) *launches = g->rem_launches.load(std::memory_order_relaxed);
-  return APPNP_OK;
-}
-
-int appnp_graph_source_block_rows(const appnp_graph* g, int* cols, int* rows_per_group,
-                                  int64_t* direct_rows) {
-  if (!g) return APPNP_EINVAL;
-  const bool built = g->rb_off != nullptr;
-  if (cols) *cols = appnp::source_block_cols(g);
-  if (rows_per_group) *rows_per_group = built ? g->rb_rg : 0;
-  if (direct_rows) *direct_rows = built ? (g->row_hi - g->row_lo) - g->rb_direct_lo : 0;
   return APPNP_OK;
 }
 

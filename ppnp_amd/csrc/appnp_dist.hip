@@ -169,7 +169,8 @@ int exchange_shards(appnp_dist* d, char* full, size_t shard_bytes, hipStream_t s
 }
 
 // Groups of remote shards in arrival order (ppnp_amd/dist.py shard_groups): sized 1, 2, 4, ...
-// from the last to arrive backwards, cut where a group would span the own shard.
+// from the last to arrive backwards, cut where a group would span the own shard, then adjacent
+// groups merged, front first, down to ceil(log2 R) groups.
 std::vector<std::pair<int, int>> shard_groups(int R, int ri) {
   std::vector<int> arrival;
   for (int s = 0; s < R; ++s)
@@ -193,6 +194,16 @@ std::vector<std::pair<int, int>> shard_groups(int R, int ri) {
       }
     }
     pos += *it;
+  }
+  int cap = 1;
+  while ((1 << cap) < R) ++cap;  // ceil(log2 R)
+  for (size_t i = 0; groups.size() > (size_t)cap && i + 2 < groups.size();) {  // not the last
+    if (groups[i].second == groups[i + 1].first) {
+      groups[i].second = groups[i + 1].second;
+      groups.erase(groups.begin() + (long)i + 1);
+    } else {
+      ++i;
+    }
   }
   return groups;
 }

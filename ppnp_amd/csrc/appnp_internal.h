@@ -59,9 +59,6 @@ struct appnp_graph {
   int32_t rb_rg = 0;            // rows per group
   int32_t rb_passes = 0;
   int32_t rb_lpe = 0;           // lanes per entry of the pass: remainder rows of 4 rb_lpe columns
-  int32_t rb_pf = 0, rb_pc = 0; // LDS sums of a row: rb_pf 16-B pieces + rb_pc floats, i.e. the
-                                // pass is sized for 4 rb_pf + rb_pc remainder columns
-  int64_t rb_direct_lo = 0;     // held rows [rb_direct_lo, rows) are gathered directly (no group)
   // shard offsets of the held rows (appnp_graph_shard_offsets): entries of held row i with a
   // column in shard s ([s sh_rows, (s+1) sh_rows)) are sh_off[s rows + i] .. sh_off[(s+1) rows + i]
   int32_t* sh_off = nullptr;    // [(sh_n + 1) * rows]
@@ -99,13 +96,8 @@ hipError_t exclusive_scan(const int32_t* cnt, int64_t rows, int32_t* out, int64_
 // lpe: lanes per entry of the remainder pass (1, 2, 4: remainder rows of 4, 8, 16 columns)
 // a_indptr / a_indices / a_nnz: the whole graph's A (the row partition's gather-locality
 // measure is taken over all of it, so every rank decides the same split)
-// cols: remainder columns the pass is sized for (0: 4 lpe)
-int graph_build_source_blocks(appnp_graph* g, int lpe, int cols, const int32_t* a_indptr,
+int graph_build_source_blocks(appnp_graph* g, int lpe, const int32_t* a_indptr,
                               const int32_t* a_indices, int64_t a_nnz, hipStream_t s);
-// columns of the remainder the built copy holds sums for (0: no copy)
-inline int source_block_cols(const appnp_graph* g) {
-  return g->rb_off ? 4 * g->rb_pf + g->rb_pc : 0;
-}
 // to_rem: out is the next remainder buffer (a unit graph stores dr o y there), not Z / dH
 hipError_t launch_remainder(const appnp_graph* g, const StepArgs& a, int epi,
                             const float* z_rem, const float* h_rem, int64_t ld_h, float* out,

@@ -433,10 +433,13 @@ class NullComm:
 def shard_groups(R: int, ri: int):
     """The pipelined step's groups of REMOTE source shards for row group ri of R: shard ranges
     [a, b) in arrival order (the exchange broadcasts roots 0 .. R-1 in turn), sized 1, 2, 4, ...
-    from the last to arrive backwards (7 remote shards: 4 + 2 + 1), and cut where a group would
-    span the rank's own shard, whose rows are not exchanged to it.  Each group's product runs as
-    soon as its last shard has landed, so after the exchange only the last group's -- one
-    shard's -- compute is left, for log2(R) extra passes over the fp32 partial instead of R - 2."""
+    from the last to arrive backwards (7 remote shards: 4 + 2 + 1), cut where a group would
+    span the rank's own shard (whose rows are not exchanged to it), and then, front first,
+    adjacent groups merged until there are at most ceil(log2 R) of them.  Each group's product
+    runs as soon as its last shard has landed, so after the exchange only the last group's --
+    one shard's -- compute is left; every group past the first costs one more pass over the
+    fp32 partial (ACC), so their number is kept at log2 R (3 on 8 ranks; one more where the own
+    shard cuts the only mergeable pair), not R - 2."""
     arrival = [s for s in range(R) if s != ri]
     sizes, left, sz = [], len(arrival), 1
     while left > 0:
@@ -453,6 +456,13 @@ def shard_groups(R: int, ri: int):
             if b is None or b != a + 1:
                 groups.append((start, a + 1))
                 start = b
+    cap = max(1, (R - 1).bit_length())  # ceil(log2 R); the last group is never merged
+    i = 0
+    while len(groups) > cap and i + 2 < len(groups):
+        if groups[i][1] == groups[i + 1][0]:
+            groups[i:i + 2] = [(groups[i][0], groups[i + 1][1])]
+        else:
+            i += 1
     return groups
 
 

@@ -44,15 +44,9 @@ def remainder_width(n: int, features: int, dtype=torch.float32) -> int:
 
 def source_block_flags(n: int, features: int, dtype=torch.float32) -> int:
     """The ``mode`` bits of the source-blocked copy for this shape (0: rows gathered whole):
-    APPNP_GRAPH_SOURCE_BLOCKS / _SB_W8 / _SB_W16 by ``remainder_width``, and for a W8 / W16 copy
-    APPNP_GRAPH_SB_COLS(r), r the remainder columns, so the pass keeps 4 r bytes of sums per row
-    and holds more rows per row pass (13-column slabs: 3 passes instead of 4 on products-synth)."""
+    APPNP_GRAPH_SOURCE_BLOCKS / _SB_W8 / _SB_W16 by ``remainder_width``."""
     w = remainder_width(n, features, dtype)
-    if not w:
-        return 0
-    r = features % 32 if features > 32 else features
-    flag = {4: _lib.GRAPH_SOURCE_BLOCKS, 8: _lib.GRAPH_SB_W8, 16: _lib.GRAPH_SB_W16}[w]
-    return flag | (_lib.GRAPH_SB_COLS(r) if w > 4 else 0)
+    return {0: 0, 4: _lib.GRAPH_SOURCE_BLOCKS, 8: _lib.GRAPH_SB_W8, 16: _lib.GRAPH_SB_W16}[w]
 
 
 def splits_rows(n: int, features: int, dtype=torch.float32) -> bool:
@@ -71,13 +65,8 @@ def source_block_layout_of(handle):
                    C.byref(launches)))
     if w.value == 0:
         return None
-    cols, rg, direct = C.c_int(), C.c_int(), C.c_int64()
-    _lib.check("appnp_graph_source_block_rows",
-               _lib.load().appnp_graph_source_block_rows(handle, C.byref(cols), C.byref(rg),
-                                                         C.byref(direct)))
     return {"width": w.value, "entries": ent.value, "value_free": bool(vf.value),
-            "row_passes": rp.value, "launches": launches.value, "cols": cols.value,
-            "rows_per_group": rg.value, "direct_rows": direct.value}
+            "row_passes": rp.value, "launches": launches.value}
 
 
 def split_layout_of(handle, f: int):

@@ -161,7 +161,9 @@ def main():
         # one broadcast per row shard and exchanged iterate (Z_0 .. Z_{K-1}), the product per
         # group of arrived shards
         bc = getattr(runner, "gloo_bcasts", None)
-        ok = ok and (bc is None or bc == K * world) and len(runner.groups) >= 1
+        # the engine's groups are dist.shard_groups' (the Python row loop's)
+        ok = ok and (bc is None or bc == K * world)
+        ok = ok and runner.groups == pdist.shard_groups(world, rank)
         extra += f" pipeline=True groups={runner.groups} bcasts={bc}"
     runner.close()
     print(f"[dist_capi] rank {rank}/{world} backend={dist.get_backend()} "

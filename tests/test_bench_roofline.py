@@ -250,22 +250,3 @@ def test_kernel_split_summarises_launches(monkeypatch):
     assert k["main"]["launches"] == 4 and k["local"]["mean"] == pytest.approx(0.2)
     assert k["remote"]["mean"] == pytest.approx(0.8) and k["xchg"]["launches"] == 2
     assert k["sum_of_kernels"] == pytest.approx((0.3 + 2 * 1.1) / 2)
-
-
-def test_packed_sums_drop_the_fourth_row_pass():
-    """sized for its 13 columns (APPNP_GRAPH_SB_COLS), the W16 pass keeps
-    52 B of sums per row, so 196 rows per wave group: 3 row passes over 2,408,448 rows and the
-    40,581 rows left (1.7 %) gathered directly; 12 columns (48 B) fit 3 passes outright.  The
-    full 16-column width keeps 4 passes (the direct share would be 20 %).  Mirrors
-    graph_build_source_blocks (appnp_blocks.hip)."""
-    assert bench.rem_row_layout(N, 4, 13) == (3, 196, N - 3 * 4096 * 196)
-    assert N - 3 * 4096 * 196 == 40_581
-    assert bench.rem_row_layout(N, 4, 12) == (3, -(-N // (3 * 4096)), 0)
-    assert bench.rem_row_layout(N, 4, 16) == (4, -(-N // (4 * 4096)), 0)
-    assert bench.rem_row_layout(N, 4) == bench.rem_row_layout(N, 4, 16)
-    assert bench.rem_row_layout(N, 1, 2) == (1, -(-N // 4096), 0)  # W4 is always 16 B a row
-    fl13 = bench.remainder_floor(N, N, NNZ, 4, 13)
-    fl16 = bench.remainder_floor(N, N, NNZ, 4, 16)
-    assert fl13["row_passes"] == 3 and fl13["direct_rows"] == 40_581
-    assert fl13["direct_lines"] == pytest.approx(NNZ * 40_581 / N)
-    assert fl13["fill_ms"] < fl16["fill_ms"]

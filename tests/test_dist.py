@@ -157,7 +157,9 @@ def test_shard_groups():
     assert shard_groups(2, 0) == [(1, 2)] and shard_groups(2, 1) == [(0, 1)]
     assert shard_groups(8, 0) == [(1, 5), (5, 7), (7, 8)]
     assert shard_groups(8, 7) == [(0, 4), (4, 6), (6, 7)]
-    assert shard_groups(8, 3) == [(0, 3), (4, 5), (5, 7), (7, 8)]
+    # the own shard cuts (0, 4) in two; merging (4, 5) + (5, 7) keeps 3 = log2(8) groups
+    assert shard_groups(8, 3) == [(0, 3), (4, 7), (7, 8)]
+    assert shard_groups(8, 5) == [(0, 5), (6, 7), (7, 8)]
     for R in range(2, 17):
         for ri in range(R):
             g = shard_groups(R, ri)
@@ -165,6 +167,7 @@ def test_shard_groups():
             assert covered == [s for s in range(R) if s != ri]
             assert all(not (a <= ri < b) for a, b in g)
             assert g[-1][1] - g[-1][0] == 1  # only one shard's compute after the exchange
+            assert len(g) <= max(1, (R - 1).bit_length()) + 1
 
 
 def test_layout_helpers():

@@ -312,13 +312,11 @@ def test_source_blocks_best_effort_fallback(ahat, tmp_path):
 @pytest.fixture(scope="module")
 def wide(adj):
     """Graphs whose source-blocked copy is laid out for 8 and 16 remainder columns (chosen by
-    Graph from the named width: 40 = 32 + 8, narrow rows of 16; a copy is sized for the
-    remainder it is named for, APPNP_GRAPH_SB_COLS, so 13 would serve at most 13 columns)."""
+    Graph from the named width: 40 = 32 + 8, narrow rows of 13)."""
     import ppnp_amd
 
     g8 = ppnp_amd.Graph.from_scipy(adj, device=DEV, features=40)
-    g16 = ppnp_amd.Graph.from_scipy(adj, device=DEV, features=16)
-    assert g16.source_block_layout()["cols"] == 16 and g8.source_block_layout()["cols"] == 8
+    g16 = ppnp_amd.Graph.from_scipy(adj, device=DEV, features=13)
     assert g8.source_block_bytes() > 0 and g16.source_block_bytes() > 0
     return {8: g8, 16: g16}
 
@@ -505,53 +503,3 @@ def test_split_from_line_aligned_h(graphs, ahat, f, ld, p):
     dH = ppnp_amd.propagate_backward(G, Hb[:, :f], 3, 0.1, p_drop=p, seed=5)
     close_fp32(dH.double().cpu().numpy(),
                O.appnp_backward(ahat, H.numpy(), 3, 0.1, p_drop=p, seed=5))
-
-
-# ---- packed sums and direct rows (APPNP_GRAPH_SB_COLS) -------------------
-
-
-def _direct_n(f):
-    """Nodes for which a W16 pass sized for f columns needs 1 row pass plus direct rows: one
-    pass holds 256 CUs x 16 waves x (160 KiB / (16 x 4 f)) rows (802,816 at f = 13); 1/16 more
-    rows than that are gathered directly (<= 1/8: the second pass is dropped)."""
-    cap = 256 * 16 * (163840 // (16 * 4 * f))
-    return cap + cap // 16
-
-
-@pytest.mark.parametrize("f,p,weighted", [(13, 0.0, False), (13, 0.3, True), (11, 0.3, False),
-                                          (9, 0.0, True)])
-def test_direct_rows_match_oracle(f, p, weighted):
-    """A W16 copy sized for f columns keeps 4 f bytes of sums per row (f = 13: 3 pieces + 1
-    float; 11: 2 + 3; 9: 2 + 1), so the rows past one row pass are gathered straight from the
-    CSR: forward (with edge dropout) and the adjoint on the value-free (unit) layout and on a
-    weighted graph (values), against the float64 oracle; the layout reports 1 pass + the rest
-    direct, and the copy serves only remainders of at most f columns."""
-    import ppnp_amd
-    from ppnp_amd import _lib
-    from ppnp_amd.graph import source_block_flags
-
-    n = _direct_n(f)
-    a = O.synth_graph(n, 2 * n, seed=20 + f)
-    if weighted:
-        a.data = (1.0 + (np.arange(a.nnz) % 7) / 4.0).astype(np.float32)
-        a = ((a + a.T) * 0.5).tocsr()
-    a.sort_indices()
-    ahat = O.calc_a_hat(a, "sym")
-    # Graph.from_csr(features=f) asks for the copy sized for f columns
-    assert source_block_flags(n, f) == _lib.GRAPH_SB_W16 | _lib.GRAPH_SB_COLS(f)
-    G = ppnp_amd.Graph.from_scipy(a, device=DEV, features=f)
-    sb = G.source_block_layout()
-    cap = 256 * 16 * (163840 // (16 * 4 * f))
-    assert sb["cols"] == f and sb["row_passes"] == 1 and sb["value_free"] == (not weighted)
-    assert sb["direct_rows"] == n - cap > 0, sb
-    assert G.remainder_cols(f) == f and G.remainder_cols(f + 1) == 0  # sized for f only
-    H = torch.from_numpy(np.random.default_rng(f).standard_normal((n, f)).astype(np.float32))
-    Z = ppnp_amd.propagate_forward(G, H.to(DEV), 3, 0.1, p_drop=p, seed=9)
-    close_fp32(Z.double().cpu().numpy(), O.appnp_propagate(ahat, H.numpy(), 3, 0.1, p_drop=p,
-                                                            seed=9))
-    dH = ppnp_amd.propagate_backward(G, H.to(DEV), 3, 0.1, p_drop=p, seed=9)
-    close_fp32(dH.double().cpu().numpy(), O.appnp_backward(ahat, H.numpy(), 3, 0.1, p_drop=p,
-                                                           seed=9))
-    # bitwise deterministic: the direct rows sum in a fixed order (a butterfly per piece)
-    assert torch.equal(Z, ppnp_amd.propagate_forward(G, H.to(DEV), 3, 0.1, p_drop=p, seed=9))
-    G.close()

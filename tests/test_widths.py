@@ -36,18 +36,14 @@ def test_no_copy(n, f, dtype):
     assert remainder_width(n, f, dtype) == 0 and not splits_rows(n, f, dtype)
 
 
-def test_source_block_flags_size_the_pass_for_the_remainder():
-    """W8 / W16 copies carry APPNP_GRAPH_SB_COLS(r): the pass keeps sums for the r columns it
-    will run, not its whole width (VERDICT r5 next #1); W4 copies need no size."""
+def test_source_block_flags():
+    """The ``mode`` bits Graph.from_csr(features=F) and the native row engine ask for."""
     from ppnp_amd import _lib
     from ppnp_amd.graph import source_block_flags
 
-    assert source_block_flags(BIG, 13) == _lib.GRAPH_SB_W16 | _lib.GRAPH_SB_COLS(13)
-    assert source_block_flags(BIG, 12) == _lib.GRAPH_SB_W16 | _lib.GRAPH_SB_COLS(12)
-    assert source_block_flags(BIG, 16) == _lib.GRAPH_SB_W16 | _lib.GRAPH_SB_COLS(16)
-    assert source_block_flags(BIG, 40) == _lib.GRAPH_SB_W8 | _lib.GRAPH_SB_COLS(8)
-    assert source_block_flags(BIG, 7) == _lib.GRAPH_SB_W8 | _lib.GRAPH_SB_COLS(7)
+    assert source_block_flags(BIG, 13) == _lib.GRAPH_SB_W16
+    assert source_block_flags(BIG, 40) == _lib.GRAPH_SB_W8
+    assert source_block_flags(BIG, 7) == _lib.GRAPH_SB_W8
     assert source_block_flags(BIG, 100) == _lib.GRAPH_SOURCE_BLOCKS
     assert source_block_flags(BIG, 3) == _lib.GRAPH_SOURCE_BLOCKS
     assert source_block_flags(BIG, 64) == 0 and source_block_flags(1000, 100) == 0
-    assert _lib.GRAPH_SB_COLS(13) == 13 << 16
