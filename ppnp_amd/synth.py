@@ -17,6 +17,8 @@ This is input synthesis, not part of the measured path.
 
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -133,7 +135,7 @@ def real_graph(name: str, device="cuda"):
     return indptr, indices
 
 
-def graph_for(workload: str, device="cuda"):
+def _make(workload: str, device):
     if workload in REAL:
         return real_graph(REAL[workload], device=device)
     n, m = CONFIGS[workload][:2]
@@ -142,6 +144,29 @@ def graph_for(workload: str, device="cuda"):
     if workload in LOCAL:
         return community_graph(n, m, SEEDS[workload], device=device)
     return uniform_graph(n, m, SEEDS.get(workload, 0), device=device)
+
+
+def graph_for(workload: str, device="cuda"):
+    """The workload's CSR (indptr, indices) on ``device``.  With PPNP_SYNTH_CACHE naming a
+    directory (the GPU test session sets one, so the products-scale tests and their child ranks
+    draw the 124 M-key graph once instead of once per module and rank), the int32 arrays are
+    kept there as ``<workload>.npz`` -- written to a temporary name and renamed, so concurrent
+    ranks never read a partial file -- and reloaded; the arrays are the generator's own either
+    way.  The bench never sets it."""
+    cache = os.environ.get("PPNP_SYNTH_CACHE")
+    if not cache:
+        return _make(workload, device)
+    path = os.path.join(cache, f"{workload}.npz")
+    if os.path.exists(path):
+        with np.load(path, allow_pickle=False) as z:
+            return (torch.from_numpy(z["indptr"]).to(device),
+                    torch.from_numpy(z["indices"]).to(device))
+    indptr, indices = _make(workload, "cpu")
+    os.makedirs(cache, exist_ok=True)
+    tmp = f"{path}.{os.getpid()}.tmp.npz"
+    np.savez(tmp, indptr=indptr.numpy(), indices=indices.numpy())
+    os.replace(tmp, path)
+    return indptr.to(device), indices.to(device)
 
 
 def features(n: int, f: int, dtype=torch.float32, device="cuda", seed: int = 0):

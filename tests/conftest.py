@@ -13,6 +13,21 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP path)")
+    # one on-disk copy of each synthetic graph for the whole session, child processes included
+    # (ppnp_amd.synth.graph_for): the products-scale tests draw the 124 M-key graph once
+    if not os.environ.get("PPNP_SYNTH_CACHE"):
+        import tempfile
+
+        os.environ["PPNP_SYNTH_CACHE"] = tempfile.mkdtemp(prefix="ppnp_synth_")
+        config._ppnp_synth_cache = os.environ["PPNP_SYNTH_CACHE"]
+
+
+def pytest_unconfigure(config):
+    d = getattr(config, "_ppnp_synth_cache", None)
+    if d:
+        import shutil
+
+        shutil.rmtree(d, ignore_errors=True)
 
 
 def load_golden(name):

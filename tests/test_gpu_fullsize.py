@@ -24,7 +24,7 @@ def products():
     from ppnp_amd import synth
 
     n, m, F, K, alpha, _ = synth.CONFIGS["products-synth"]
-    indptr, indices = synth.uniform_graph(n, m, synth.SEEDS["products-synth"], device=DEV)
+    indptr, indices = synth.graph_for("products-synth", device=DEV)  # the session's copy
     return dict(n=n, F=F, K=K, alpha=alpha, indptr=indptr, indices=indices)
 
 

@@ -80,3 +80,19 @@ def test_features_are_cpu_generator_draws():
     H = synth.features(100, 7, device="cpu")
     g = torch.Generator().manual_seed(0)
     assert torch.equal(H, torch.randn(100, 7, generator=g))
+
+
+def test_graph_cache_returns_the_generator_arrays(tmp_path, monkeypatch):
+    """PPNP_SYNTH_CACHE (set by tests/conftest.py for the GPU session and its child ranks): the
+    first call writes the workload's CSR, later calls read it back, and both equal the
+    generator's own arrays."""
+    from ppnp_amd import synth
+
+    monkeypatch.delenv("PPNP_SYNTH_CACHE", raising=False)
+    ip0, ix0 = synth.graph_for("pubmed-synth", device="cpu")
+    monkeypatch.setenv("PPNP_SYNTH_CACHE", str(tmp_path))
+    ip1, ix1 = synth.graph_for("pubmed-synth", device="cpu")
+    assert (tmp_path / "pubmed-synth.npz").exists()
+    ip2, ix2 = synth.graph_for("pubmed-synth", device="cpu")
+    for a, b, c in ((ip0, ip1, ip2), (ix0, ix1, ix2)):
+        assert torch.equal(a, b) and torch.equal(a, c) and a.dtype == c.dtype == torch.int32
