@@ -122,7 +122,7 @@ __device__ __forceinline__ void frag_store(T* p, const float (&x)[V], int rem, b
 template <typename T, int V, int EPI, bool TAIL>
 __device__ __forceinline__ void epilogue(const StepArgs& a, int64_t row, int col0,
                                          const float (&acc)[V], const float (&hv)[V],
-                                         int rem) {
+                                         const float (&pv)[V], int rem) {
   float y[V];
 #pragma unroll
   for (int v = 0; v < V; ++v) y[v] = a.scale * acc[v];
@@ -133,40 +133,48 @@ __device__ __forceinline__ void epilogue(const StepArgs& a, int64_t row, int col
                            a.nt & 4);
   } else if constexpr (EPI == EPI_BWD) {
     if (a.out) frag_store<T, V, TAIL>(static_cast<T*>(a.out) + row * a.ld_out + col0, y, rem);
-    T* d = static_cast<T*>(a.aux) + row * a.ld_aux + col0;
     float dv[V];
-    frag_load<T, V, TAIL>(d, dv, rem, row + 1 < a.n_rows);
 #pragma unroll
-    for (int v = 0; v < V; ++v) dv[v] = fmaf(a.alpha, y[v], dv[v]);
-    frag_store<T, V, TAIL>(d, dv, rem);
+    for (int v = 0; v < V; ++v) dv[v] = fmaf(a.alpha, y[v], pv[v]);
+    frag_store<T, V, TAIL>(static_cast<T*>(a.aux) + row * a.ld_aux + col0, dv, rem);
   } else if constexpr (EPI == EPI_PARTIAL) {
     frag_store<float, V, TAIL>(static_cast<float*>(a.out) + row * a.ld_out + col0, y, rem);
   } else if constexpr (EPI == EPI_ACCUM) {
-    float* o = static_cast<float*>(a.out) + row * a.ld_out + col0;
-    float pv[V];
-    frag_load<float, V, TAIL>(o, pv, rem, row + 1 < a.n_rows);
 #pragma unroll
     for (int v = 0; v < V; ++v) y[v] += pv[v];
-    frag_store<float, V, TAIL>(o, y, rem);
+    frag_store<float, V, TAIL>(static_cast<float*>(a.out) + row * a.ld_out + col0, y, rem);
   } else {  // EPI_FINISH
-    float pv[V];
-    frag_load<float, V, TAIL>(static_cast<const float*>(a.aux) + row * a.ld_aux + col0, pv, rem,
-                              row + 1 < a.n_rows);
 #pragma unroll
     for (int v = 0; v < V; ++v) y[v] = fmaf(a.alpha, hv[v], y[v] + pv[v]);
     frag_store<T, V, TAIL>(static_cast<T*>(a.out) + row * a.ld_out + col0, y, rem);
   }
 }
 
+// The row's epilogue operands, loaded when the row starts so their latency hides under the
+// gathers: H (forward, finish), dH (adjoint, in `aux`) and the fp32 partial of the
+// row-partition steps (accumulate: the partial in `out`; finish: the one in `aux`).
 template <typename T, int V, int EPI, bool TAIL>
 __device__ __forceinline__ void load_h(const StepArgs& a, int64_t row, int col0, float (&hv)[V],
-                                       int rem) {
+                                       float (&pv)[V], int rem) {
   if constexpr (EPI == EPI_FWD || EPI == EPI_FINISH) {
     frag_load<T, V, TAIL>(static_cast<const T*>(a.h) + row * a.ld_h + col0, hv, rem,
                           row + 1 < a.n_rows, a.nt & 2);
   } else {
 #pragma unroll
     for (int v = 0; v < V; ++v) hv[v] = 0.0f;
+  }
+  if constexpr (EPI == EPI_BWD) {
+    frag_load<T, V, TAIL>(static_cast<const T*>(a.aux) + row * a.ld_aux + col0, pv, rem,
+                          row + 1 < a.n_rows);
+  } else if constexpr (EPI == EPI_ACCUM) {
+    frag_load<float, V, TAIL>(static_cast<const float*>(a.out) + row * a.ld_out + col0, pv, rem,
+                              row + 1 < a.n_rows);
+  } else if constexpr (EPI == EPI_FINISH) {
+    frag_load<float, V, TAIL>(static_cast<const float*>(a.aux) + row * a.ld_aux + col0, pv, rem,
+                              row + 1 < a.n_rows);
+  } else {
+#pragma unroll
+    for (int v = 0; v < V; ++v) pv[v] = 0.0f;
   }
 }
 
@@ -182,8 +190,8 @@ __device__ __forceinline__ void wave_row(const StepArgs& a, int64_t row, int lan
   const T* __restrict__ zin = static_cast<const T*>(a.zin);
   const int beg = a.row_ptr[row];
   const int end = row_end_of(a, row);
-  float hv[V];
-  if (sub == 0 && fact) load_h<T, V, EPI, TAIL>(a, row, col0, hv, rem);
+  float hv[V], pv[V];
+  if (sub == 0 && fact) load_h<T, V, EPI, TAIL>(a, row, col0, hv, pv, rem);
   float acc[V];
 #pragma unroll
   for (int v = 0; v < V; ++v) acc[v] = 0.0f;
@@ -238,7 +246,7 @@ __device__ __forceinline__ void wave_row(const StepArgs& a, int64_t row, int lan
 #pragma unroll
     for (int v = 0; v < V; ++v) acc[v] += __shfl_xor(acc[v], off);
   }
-  if (sub == 0 && fact) epilogue<T, V, EPI, TAIL>(a, row, col0, acc, hv, rem);
+  if (sub == 0 && fact) epilogue<T, V, EPI, TAIL>(a, row, col0, acc, hv, pv, rem);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -302,8 +310,8 @@ __global__ __launch_bounds__(kBlock) void k_step_narrow(StepArgs a) {
     const int beg = a.row_ptr[row];
     const int end = row_end_of(a, row);
     if (a.heavy && end - beg > a.heavy_thr) continue;
-    float hv[V];
-    if (fact) load_h<T, V, EPI, TAIL>(a, row, col0, hv, rem);
+    float hv[V], pv[V];
+    if (fact) load_h<T, V, EPI, TAIL>(a, row, col0, hv, pv, rem);
     float acc[V];
 #pragma unroll
     for (int v = 0; v < V; ++v) acc[v] = 0.0f;
@@ -344,7 +352,7 @@ __global__ __launch_bounds__(kBlock) void k_step_narrow(StepArgs a) {
         for (int v = 0; v < V; ++v) acc[v] = fmaf(w[u], z[u][v], acc[v]);
       }
     }
-    if (fact) epilogue<T, V, EPI, TAIL>(a, row, col0, acc, hv, rem);
+    if (fact) epilogue<T, V, EPI, TAIL>(a, row, col0, acc, hv, pv, rem);
   }
 }
 

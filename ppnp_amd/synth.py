@@ -103,7 +103,12 @@ def chung_lu_graph(n: int, m: int, seed: int, exponent: float = 3.2, device="cud
     w = np.arange(1, n + 1, dtype=np.float64) ** (-1.0 / (exponent - 1.0))
     cdf = np.cumsum(w)
     cdf /= cdf[-1]
-    ends = np.minimum(np.searchsorted(cdf, rng.random((2, m))), n - 1)
+    # numpy's searchsorted semantics (first i with cdf[i] >= u) on torch's threads: the same
+    # indices, ~10x faster for 124 M lookups
+    u = torch.from_numpy(rng.random((2, m)))
+    ends = torch.searchsorted(torch.from_numpy(cdf), u.reshape(-1)).reshape(2, m).numpy()
+    del u
+    ends = np.minimum(ends, n - 1)
     perm = rng.permutation(n)
     return _csr_from_pairs(perm[ends[0]], perm[ends[1]], n, device)
 

@@ -17,6 +17,7 @@ import argparse
 import os
 import sys
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -59,6 +60,10 @@ def main():
                    help="with --oracle-torch: rank 0 alone runs the oracle and sends every rank "
                         "its block (gloo point to point), instead of every rank running it -- "
                         "8 products-scale fp64 oracles would not fit the box's CPU share")
+    p.add_argument("--h-seed", type=int, default=1,
+                   help="seed of H (synth.features); with --oracle-torch on a workload the "
+                        "reference is shared through tests/ref_cache.py, so seed 0 reads the "
+                        "session's products reference instead of recomputing it")
     p.add_argument("--pipeline", default="auto", choices=["auto", "on", "off"],
                    help="the pipelined exchange (one broadcast per row shard, the product per "
                         "group of arrived shards): auto = whenever it applies")
@@ -91,7 +96,7 @@ def main():
     else:
         a.K = 10 if a.K is None else a.K
         indptr, indices = synth.uniform_graph(a.n, a.m, 7, device=dev)
-    H = synth.features(a.n, a.f, device=dev, seed=1)
+    H = synth.features(a.n, a.f, device=dev, seed=a.h_seed)
     if rank == a.sb_oom_rank:
         _require_test_library()
         os.environ["APPNP_SB_TEST_OOM"] = "1"
@@ -105,27 +110,24 @@ def main():
     if a.oracle_torch and a.oracle_rank0:
         if dist.get_backend() != "gloo":
             raise SystemExit("--oracle-rank0 sends the blocks over gloo")
-        ref = _torch_oracle(a, indptr, indices, H, dev, threads=16) if rank == 0 else None
+        ref = (torch.from_numpy(_torch_oracle(a, indptr, indices, H, dev, threads=16))
+               if rank == 0 else None)
         block, ref_max = _send_blocks(ref, (runner.lo, runner.hi, runner.f_lo, runner.f_hi),
                                       rank, world)
         del ref
+    elif a.oracle_torch:
+        ref = _torch_oracle(a, indptr, indices, H, dev, threads=8, mmap=True)
+        block = torch.from_numpy(np.array(ref[runner.lo:runner.hi, runner.f_lo:runner.f_hi]))
+        ref_max = float(np.abs(ref).max())
+        del ref
+    elif a.oracle:
+        ref = _fp64_oracle(a, indptr, indices, H, rank)
+        block = torch.from_numpy(np.array(ref[runner.lo:runner.hi, runner.f_lo:runner.f_hi]))
+        ref_max = float(np.abs(ref).max())
+        del ref
     else:
-        if a.oracle_torch:
-            ref = _torch_oracle(a, indptr, indices, H, dev, threads=8)
-        elif a.oracle:
-            import numpy as np
-            import scipy.sparse as sp
-
-            from oracle import ppnp_oracle as O
-
-            adj = sp.csr_matrix((np.ones(indices.numel(), dtype=np.float32),
-                                 indices.cpu().numpy(), indptr.cpu().numpy()), shape=(a.n, a.n))
-            ref = torch.from_numpy(O.appnp_propagate(O.calc_a_hat(adj, "sym"),
-                                                     H.double().cpu().numpy(), a.K, a.alpha,
-                                                     p_drop=a.p_drop, seed=5)).to(dev)
-        else:
-            G = ppnp_amd.Graph.from_csr(indptr, indices, None, a.n, device=dev)
-            ref = ppnp_amd.propagate_forward(G, H, a.K, a.alpha, p_drop=a.p_drop, seed=5)
+        G = ppnp_amd.Graph.from_csr(indptr, indices, None, a.n, device=dev)
+        ref = ppnp_amd.propagate_forward(G, H, a.K, a.alpha, p_drop=a.p_drop, seed=5)
         block = ref[runner.lo:runner.hi, runner.f_lo:runner.f_hi]
         ref_max = ref.abs().max().item()
     got = Z if Z.device == block.device else Z.cpu()
@@ -150,19 +152,53 @@ def main():
     sys.exit(1 if flag.item() else 0)
 
 
-def _torch_oracle(a, indptr, indices, H, dev, threads):
-    """The oracle's float64 torch.sparse CPU loop over the device A_hat of a whole-graph build."""
-    import ppnp_amd
+def _fp64_oracle(a, indptr, indices, H, rank):
+    """The float64 oracle (oracle/ppnp_oracle.py appnp_propagate over calc_a_hat, scipy) of this
+    run's graph, H, K, alpha and dropout.  With the session's cache (tests/ref_cache.py) rank 0
+    computes it and the other ranks wait at a barrier and map it, so ranks do not compete for the
+    box's CPU share and later runs of the same case read it back."""
+    import scipy.sparse as sp
+
+    import ref_cache
     from oracle import ppnp_oracle as O
 
-    G = ppnp_amd.Graph.from_csr(indptr, indices, None, a.n, device=dev)
-    rp, col, val, _ = G.csr()
-    A = torch.sparse_csr_tensor(rp.cpu().long(), col.cpu().long(), val.cpu().double(),
-                                size=(a.n, a.n))
-    G.close()
-    del rp, col, val
-    torch.set_num_threads(max(1, min(threads, len(os.sched_getaffinity(0)))))
-    return O.appnp_propagate_torch_cpu(A, H.cpu().double(), a.K, a.alpha)
+    def build():
+        adj = sp.csr_matrix((np.ones(indices.numel(), dtype=np.float32),
+                             indices.cpu().numpy(), indptr.cpu().numpy()), shape=(a.n, a.n))
+        return O.appnp_propagate(O.calc_a_hat(adj, "sym"), H.double().cpu().numpy(), a.K,
+                                 a.alpha, p_drop=a.p_drop, seed=5)
+
+    if not os.environ.get("PPNP_SYNTH_CACHE"):
+        return build()
+    graph = a.workload or f"uniform-n{a.n}-m{a.m}-s7"
+    tag = f"{graph}-f{a.f}-h{a.h_seed}-K{a.K}-a{a.alpha}-p{a.p_drop}-s5"
+    if rank == 0:
+        ref_cache.reference(tag, build, mmap=True)
+    dist.barrier()
+    return ref_cache.reference(tag, build, mmap=True)
+
+
+def _torch_oracle(a, indptr, indices, H, dev, threads, mmap=False):
+    """The oracle's float64 torch.sparse CPU loop over the device A_hat of a whole-graph build,
+    as a float64 numpy array; a workload's is shared through tests/ref_cache.py (the same tag as
+    tests/test_gpu_configs.py's products_ref fixture)."""
+    import ppnp_amd
+    import ref_cache
+    from oracle import ppnp_oracle as O
+
+    def build():
+        G = ppnp_amd.Graph.from_csr(indptr, indices, None, a.n, device=dev)
+        rp, col, val, _ = G.csr()
+        A = torch.sparse_csr_tensor(rp.cpu().long(), col.cpu().long(), val.cpu().double(),
+                                    size=(a.n, a.n))
+        G.close()
+        del rp, col, val
+        torch.set_num_threads(max(1, min(threads, len(os.sched_getaffinity(0)))))
+        return O.appnp_propagate_torch_cpu(A, H.cpu().double(), a.K, a.alpha).numpy()
+
+    if not a.workload:
+        return build()
+    return ref_cache.reference(f"{a.workload}-h{a.h_seed}-K{a.K}-a{a.alpha}", build, mmap=mmap)
 
 
 def _send_blocks(ref, mine, rank, world):

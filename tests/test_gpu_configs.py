@@ -15,7 +15,7 @@ compares the WHOLE Z_K with an oracle computed on the CPU from the same A and H:
 * config 4 row-partitioned over 2 and 4 ranks sharing the one GPU (gloo exchange, with and
   without the overlapped local/remote split), each rank against the float64 oracle:
   tests/dist_worker.py launched by torch.distributed.run as fresh child processes;
-* config 5 row-partitioned: products-synth over 2 ranks (K = 2) and over the north_star's 8
+* config 5 row-partitioned: products-synth over 2 ranks and over the north_star's 8
   ranks (all K = 10 iterations, rank 0's float64 oracle sent to every rank).
 """
 
@@ -118,6 +118,23 @@ def products():
     G.close()
 
 
+@pytest.fixture(scope="module")
+def products_ref(products):
+    """The float64 torch.sparse loop of the products fixture's A_hat on its H (seed 0), all K
+    iterations: computed once per session (tests/ref_cache.py) and shared by the forward, the
+    adjoint, the column slab and the row-partition workers."""
+    import ref_cache
+
+    _, H, K, alpha, a, _ = products
+    ref = ref_cache.reference(_ref_tag("products-synth", 0, K, alpha),
+                       lambda: O.appnp_propagate_torch_cpu(a, H.cpu().double(), K, alpha).numpy())
+    return torch.from_numpy(ref)
+
+
+def _ref_tag(workload, h_seed, K, alpha):
+    return f"{workload}-h{h_seed}-K{K}-a{alpha}"
+
+
 def test_products_a_hat_matches_calc_a_hat(products):
     """The device CSR build at products scale (126 M entries of A_hat) against the oracle's
     calc_a_hat (helpers.py:58-66) on the same A: row pointers and column indices bit-exact,
@@ -137,27 +154,26 @@ def test_products_a_hat_matches_calc_a_hat(products):
     assert rel <= 2.0 ** -51, rel
 
 
-def test_products_k10_matches_oracle(products):
+def test_products_k10_matches_oracle(products, products_ref):
     """Config 5 at full size, K = 10, on the split-row path -- every one of the 244.9 M values
     against the float64 torch.sparse CPU loop of the same A_hat (helpers.py:58-66)."""
     import ppnp_amd
 
-    G, H, K, alpha, a, _ = products
+    G, H, K, alpha, _, _ = products
     Z = ppnp_amd.propagate_forward(G, H, K, alpha).cpu()
-    _check_full(Z, O.appnp_propagate_torch_cpu(a, H.cpu().double(), K, alpha))
+    _check_full(Z, products_ref)
 
 
-def test_products_k10_backward_matches_oracle(products):
+def test_products_k10_backward_matches_oracle(products, products_ref):
     """The adjoint at full size on the split path (appnp_propagate_bwd: main-column chain plus
     the remainder pass with its adjoint epilogue).  Without dropout APPNP_K is a polynomial in
-    the symmetric A_hat, so J^T dZ = APPNP_K(dZ): the float64 forward loop is its oracle."""
+    the symmetric A_hat, so J^T dZ = APPNP_K(dZ): the float64 forward loop is its oracle, and
+    with dZ = H it is the forward's reference."""
     import ppnp_amd
 
-    G, H, K, alpha, a, _ = products
-    g = torch.Generator(device="cpu").manual_seed(11)
-    dZ = torch.randn(H.shape, generator=g, dtype=torch.float32)
-    dH = ppnp_amd.propagate_backward(G, dZ.to(DEV), K, alpha).cpu()
-    _check_full(dH, O.appnp_propagate_torch_cpu(a, dZ.double(), K, alpha))
+    G, H, K, alpha, _, _ = products
+    dH = ppnp_amd.propagate_backward(G, H, K, alpha).cpu()
+    _check_full(dH, products_ref)
 
 
 def test_products_k10_bf16_matches_oracle(products):
@@ -174,20 +190,21 @@ def test_products_k10_bf16_matches_oracle(products):
     assert float((Z.argmax(1) == ref.argmax(1)).double().mean()) >= 0.98
 
 
-def test_products_col8_slab_matches_oracle(products):
+def test_products_col8_slab_matches_oracle(products, products_ref):
     """The 13-column slab of F = 100 on 8 column ranks (rank 0 of the exchange-free 8-GPU layout)
     on its W16 copy (4 row passes, piece-major LDS sums), every value of Z_K, K = 10, against the
-    float64 torch.sparse loop of the same A_hat."""
+    float64 torch.sparse loop of the same A_hat (columns are independent: the first 13 columns
+    of the whole reference)."""
     import ppnp_amd
 
-    _, H, K, alpha, a, adj = products
+    _, H, K, alpha, _, adj = products
     G = ppnp_amd.Graph.from_scipy(adj, device=DEV, features=13)
     sb = G.source_block_layout()
     assert (sb["width"], sb["row_passes"]) == (16, 4), sb
     assert G.remainder_cols(13) == 13
     H13 = H[:, :13].contiguous()
     Z = ppnp_amd.propagate_forward(G, H13, K, alpha).cpu()
-    _check_full(Z, O.appnp_propagate_torch_cpu(a, H13.cpu().double(), K, alpha))
+    _check_full(Z, products_ref[:, :13])
     G.close()
 
 
@@ -417,16 +434,17 @@ def test_row_partition_split_rows_matches_oracle(ranks, extra):
 @pytest.mark.parametrize("extra", [["--overlap"], []])
 def test_products_row_partition_matches_oracle(extra):
     """the north_star's row partition on config 5's own workload -- products-synth
-    (2,449,029 x 100, 126 M nonzeros) over 2 ranks sharing the GPU (gloo exchange), K = 2, every
+    (2,449,029 x 100, 126 M nonzeros) over 2 ranks sharing the GPU (gloo exchange), K = 10, every
     rank on the split rows of its held rows (3 gathered lines + the L2-blocked remainder pass,
     both parts exchanged), with and without the overlapped local/remote split.  Each rank's
     block of Z_K against the float64 torch.sparse loop over the device A_hat, which
-    test_products_a_hat_matches_calc_a_hat pins to calc_a_hat (helpers.py:58-66)."""
+    test_products_a_hat_matches_calc_a_hat pins to calc_a_hat (helpers.py:58-66) -- the
+    session's products reference on H of seed 0 (tests/ref_cache.py)."""
     env = dict(os.environ, PPNP_DIST_BACKEND="gloo", PYTHONPATH=ROOT, OMP_NUM_THREADS="8")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
            os.path.join(ROOT, "tests", "dist_worker.py"), "--layout", "row", "--workload",
-           "products-synth", "--K", "2", "--oracle-torch", "--expect-split", "4", *extra]
+           "products-synth", "--h-seed", "0", "--oracle-torch", "--expect-split", "4", *extra]
     proc = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=400)
     assert proc.returncode == 0, proc.stdout[-3000:] + proc.stderr[-3000:]
     res = _rank_results(proc.stdout, "dist_worker")
@@ -443,8 +461,8 @@ def test_products_eight_rank_row_partition_k10_matches_oracle():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=8",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
            os.path.join(ROOT, "tests", "dist_worker.py"), "--layout", "row", "--workload",
-           "products-synth", "--oracle-torch", "--oracle-rank0", "--expect-split", "4",
-           "--overlap"]
+           "products-synth", "--h-seed", "0", "--oracle-torch", "--oracle-rank0",
+           "--expect-split", "4", "--overlap"]
     proc = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=400)
     assert proc.returncode == 0, proc.stdout[-3000:] + proc.stderr[-3000:]
     res = _rank_results(proc.stdout, "dist_worker")
