@@ -968,9 +968,12 @@ def main(argv=None):
         if world > 1 and layout.rows > 1:
             pdist.ensure_data_group(data_backend, dev)  # collective; RCCL comes up here
         t1 = time.perf_counter()
+        kw = dict(emu)
+        if "comm" in kw:  # emulated rank: pipelines only where the real exchange could
+            kw["comm"] = pdist.NullComm(broadcast=not pdist.relayed(layout, exchange))
         runner = pdist.PartitionedAPPNP.create(indptr, indices, n, H, K, alpha, dev,
                                                layout=layout, overlap=overlap,
-                                               exchange=exchange, pipeline=pipeline, **emu)
+                                               exchange=exchange, pipeline=pipeline, **kw)
         torch.cuda.synchronize()
         t_build = time.perf_counter() - t1
         try:

@@ -418,16 +418,28 @@ class MultipathComm:
 
 
 class NullComm:
-    """No exchange (emulation of one rank on one GPU; the gathered rows keep stale data)."""
+    """No exchange (emulation of one rank on one GPU; the gathered rows keep stale data).
+    ``broadcast``: whether the exchange it stands in for can broadcast row shards (the relayed
+    exchange cannot), which decides whether the emulated rank pipelines like the real one."""
 
     name = "none"
-    supports_broadcast = True
+
+    def __init__(self, broadcast: bool = True):
+        self.supports_broadcast = broadcast
 
     def all_gather_rows(self, full, shard_rows, async_op):
         return None
 
     def broadcast_rows(self, full, shard_rows, root, async_op):
         return None
+
+
+def relayed(layout: Layout, exchange: str) -> bool:
+    """Whether ``exchange`` runs as MultipathComm's relayed all-gather on ``layout`` (R x C with
+    R, C > 1).  The relay moves whole iterates and cannot broadcast single row shards, so such a
+    rank never pipelines (the autotuner then measures an R x C layout both ways: relayed under
+    'multipath', pipelined under 'group')."""
+    return exchange == "multipath" and layout.rows > 1 and layout.cols > 1
 
 
 def shard_groups(R: int, ri: int):
@@ -569,8 +581,7 @@ class PartitionedAPPNP:
             widths = None if split else [
                 col_range(f, layout.cols, c)[1] - col_range(f, layout.cols, c)[0]
                 for c in range(layout.cols)]
-            comm = (MultipathComm(layout, rank, widths)
-                    if exchange == "multipath" and layout.rows > 1 and layout.cols > 1
+            comm = (MultipathComm(layout, rank, widths) if relayed(layout, exchange)
                     else _TorchComm(layout, rank))
         step_fn = step_fn or _hip_step
         obj = cls(layout, rank, n, f, K, alpha, graph, H_slab, f_lo, f_hi, bufs, shard, lo, hi,
