@@ -1,5 +1,5 @@
 """CPU: which source-blocked copy ``Graph.from_csr(features=F)`` asks for (graph.remainder_width),
-the host half of appnp_capi.hip's ``remainder_cols`` rule (DESIGN.md sections 4.2 and 9):
+the host half of appnp_capi.hip's ``remainder_cols`` rule:
 
 * fp32 rows of F = 32q + r features, 1 <= r <= 8, beside whole lines: the narrowest copy that
   holds r (W4 for r <= 4, W8 for 5-8); wider remainders keep whole rows;

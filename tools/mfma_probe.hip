@@ -6,7 +6,7 @@
 //      T = 16-row tiles per wave, WPC = waves per CU, U = quads in flight, br = log2 source
 //      rows per block
 //
-// Why (DESIGN.md section 9, profiles/r2_blk_probe.txt): the LDS-accumulator pass (blk_probe
+// Why (DESIGN.md Appendix A.9, profiles/r2_blk_probe.txt): the LDS-accumulator pass (blk_probe
 // k_blk, W = 16) needs 4 row passes on products-synth (160 KB of LDS per CU holds 2,400 rows of
 // 64 B), and every row pass re-fetches the whole [n, 16] table into every XCD's L2: 1.89 ms
 // per pass against 0.68 ms for the one-pass W = 4 form.  The register file is 3.2x the LDS
