@@ -178,14 +178,16 @@ def test_products_k10_backward_matches_oracle(products, products_ref):
 
 def test_products_k10_bf16_matches_oracle(products):
     """bf16 storage with fp32 accumulation at products scale (whole 200-B rows: the split path
-    is fp32-only), against the float64 loop on the bf16-rounded H: the bf16 bar of DESIGN.md 2."""
+    is fp32-only), against the oracle's torch.sparse loop on the bf16-rounded H: the bf16 bar of
+    DESIGN.md 2.  The loop runs in float32 (its ~1e-7 relative error is five orders below the
+    2e-2 bar, and it takes half the float64 loop's time)."""
     import ppnp_amd
 
     G, H, K, alpha, a, _ = products
     Hb = H.to(torch.bfloat16)
     assert G.split_point(int(H.shape[1]), torch.bfloat16) == 0
     Z = ppnp_amd.propagate_forward(G, Hb, K, alpha).float().cpu().double()
-    ref = O.appnp_propagate_torch_cpu(a, Hb.float().cpu().double(), K, alpha)
+    ref = O.appnp_propagate_torch_cpu(a.to(torch.float32), Hb.float().cpu(), K, alpha).double()
     assert float((Z - ref).abs().max()) <= 2e-2 * float(ref.abs().max())
     assert float((Z.argmax(1) == ref.argmax(1)).double().mean()) >= 0.98
 
@@ -208,12 +210,15 @@ def test_products_col8_slab_matches_oracle(products, products_ref):
     G.close()
 
 
-def test_products_powerlaw_k10_matches_oracle():
+def test_products_powerlaw_matches_oracle():
     """The Chung-Lu power-law graph with products' node and edge counts (hub rows: the heavy /
-    hub lists of the main SpMM and long runs in the remainder pass) at full size, K = 10."""
+    hub lists of the main SpMM and long runs in the remainder pass) at full size.  K = 4: every
+    launch shape of K = 10 (first, middle and last iteration; hub rows in each) at 40 % of the
+    oracle's time -- K = 10 itself is pinned on products-synth."""
     import ppnp_amd
 
-    G, H, K, alpha, a, _ = _products_case("products-powerlaw")
+    G, H, _, alpha, a, _ = _products_case("products-powerlaw")
+    K = 4
     try:
         Z = ppnp_amd.propagate_forward(G, H, K, alpha).cpu()
     finally:
