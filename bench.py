@@ -445,7 +445,8 @@ def roofline(*, n, rows, nnz, F_local, esz, avg_iter_ms, fs, r, lpe, exchange_in
             "basis": f"max of: {lines:.4g} line requests per iteration at "
                      f"{GATHER_LINE_CEILING} G lines/s"
                      + (f" + the W{width} remainder pass's count floor for {nnz:.4g} "
-                        f"nonzeros ({rem['row_passes']} row passes; remainder_pass_floor)"
+                        f"nonzeros ({rem['row_passes']} row "
+                        f"pass{'' if rem['row_passes'] == 1 else 'es'}; remainder_pass_floor)"
                         if r else "")
                      + f"; exchange {exchange_in_bytes / 1e6:.4g} MB in at "
                        f"{XGMI_IN_GBS:.0f} GB/s; B_iter at the HBM peak",
