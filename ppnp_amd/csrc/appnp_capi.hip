@@ -147,6 +147,7 @@ StepArgs base_args(const appnp_graph* g, int64_t f, float alpha) {
   a.val = g->val;
   a.n_rows = g->row_hi - g->row_lo;
   a.nnz = g->nnz_hat;
+  a.nnz_rows = g->nnz_hat;  // a step over part of the rows' entries overrides nnz only
   a.zin_rows = g->n;
   a.row_lo = g->row_lo;
   a.f = (int32_t)f;

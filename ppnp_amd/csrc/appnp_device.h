@@ -35,6 +35,8 @@ struct StepArgs {
   int64_t ld_in, ld_h, ld_out, ld_aux;
   int64_t n_rows;          // rows held
   int64_t nnz;             // entries of those rows (< 0: unknown); picks the row shape
+  int64_t nnz_rows;        // entries of the whole rows when nnz counts a part of them (a shard
+                           // range, the LOCAL / REMOTE half); 0: nnz
   int64_t zin_rows;        // rows of zin (its last row is never over-read)
   int64_t row_lo;          // global index of local row 0 (hash key only)
   uint64_t mkey;           // per-iteration dropout key = splitmix64(seed + (k+1)*golden)

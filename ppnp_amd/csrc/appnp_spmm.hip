@@ -507,8 +507,17 @@ hipError_t launch_step(int dtype, int epi, int V, const StepArgs& a_in, hipStrea
   // (arxiv-synth, 14.8 a row): 1, 3 % faster than 2.  Small graphs with hub rows (latency
   // regime, wave per row because of them): 8, so the longest row -- which sets the launch
   // time -- takes few dependent rounds (Cora-ML 9.4 -> 5.8 us, Citeseer 5.4 -> 3.9 us).
+  // Short rows keep 1 when they are whole rows, but not when they are a range of long rows (the
+  // LOCAL half of a row-partitioned step, the shard groups of a pipelined one: 6-26 entries a
+  // row of products-synth's 51.5): there 2 is 3-10 % faster (profiles/r6_row8_pipeline.txt,
+  // h3_*), while arxiv-synth's whole 14.8-entry rows keep 1 (2 % faster; h4_*).
+  const int64_t whole = a.nnz_rows > 0 ? a.nnz_rows : a.nnz;
+  const bool long_whole = whole >= (int64_t)kWideAvgRow * a.n_rows;
   static const int uw_env = tuning_env("APPNP_UW", -1);  // tuning override (1, 2, 4, 8)
-  const int uw = uw_env > 0 ? uw_env : (latency && heavy_rows) ? 8 : (!latency && long_rows) ? 2 : 1;
+  const int uw = uw_env > 0                ? uw_env
+                 : (latency && heavy_rows) ? 8
+                 : (!latency && (long_rows || long_whole)) ? 2
+                                                           : 1;
   // cache policy of the streams (StepArgs::nt); APPNP_NT overrides for measurement
   // entries in flight per row of the narrow kernels: 8 in the latency regime, where a row's
   // dependent rounds set the launch time (pubmed-synth 5.77 -> 5.24 us, cora-sized uniform
