@@ -33,6 +33,7 @@ else
   add row4 --layout row --overlap --emulate 4:0
   add r2c4 --layout 2x4 --overlap --emulate 8:0
   add r4c2 --layout 4x2 --overlap --emulate 8:0
+  add r4c2g --layout 4x2 --overlap --exchange group --emulate 8:0
   add row8 --layout row --overlap --emulate 8:0
   add row8r3 --layout row --overlap --emulate 8:3
   add row8np --layout row --overlap --pipeline off --emulate 8:0
