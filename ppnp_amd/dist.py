@@ -533,7 +533,9 @@ class PartitionedAPPNP:
         width = f_hi - f_lo
         esz = H.element_size()
         ld = line_ld(width, esz)
-        overlap = bool(overlap and layout.rows > 1)
+        # the LOCAL / REMOTE halves and the pipelined shard steps keep an fp32 partial of fp32
+        # rows (appnp_step: APPNP_ENOTSUP otherwise): bf16 storage exchanges without overlap
+        overlap = bool(overlap and layout.rows > 1 and H.dtype == torch.float32)
         if graph_fn is None:
             from .graph import Graph
 

@@ -339,3 +339,21 @@ def test_split_agreement_needs_equal_parts(splits, agreed):
                        start_method="spawn")
     res = dict(q.get() for _ in range(4))
     assert all(v == agreed for v in res.values()), res
+
+
+def test_bf16_row_layout_exchanges_without_overlap():
+    """The LOCAL / REMOTE halves and the pipelined shard steps are fp32-only (appnp_step returns
+    APPNP_ENOTSUP for bf16 halves), so a bf16 row layout asked to overlap runs the plain
+    exchange-then-step loop instead of failing in its first step."""
+    from ppnp_amd.dist import Layout, NullComm, PartitionedAPPNP
+
+    a_hat = O.calc_a_hat(O.synth_graph(N, 4 * N, seed=5), "sym")
+    H = torch.zeros(N, F, dtype=torch.bfloat16)
+    for dtype, want in ((torch.bfloat16, False), (torch.float32, True)):
+        r = PartitionedAPPNP.create(None, None, N, H.to(dtype), K, ALPHA, "cpu",
+                                    layout=Layout(4, 1), overlap=True, rank=1, world=4,
+                                    comm=NullComm(),
+                                    graph_fn=lambda lo, hi, ov: _FakeGraph(a_hat, lo, hi, ov),
+                                    step_fn=_oracle_step)
+        assert r.overlap is want and r.pipeline is want, (dtype, r.overlap, r.pipeline)
+
