@@ -415,6 +415,25 @@ def test_native_row_engine_rccl_callback_one_rank(backend):
     assert len(lines) == 1 and "rccl_callback rc=0" in lines[0] and lines[0].endswith("OK"), lines
 
 
+@pytest.mark.parametrize("f", [20, 50])
+def test_pipelined_narrow_and_two_line_rows_match_oracle(f):
+    """The pipelined shard steps on rows narrower than a wavefront's slab: F = 20 runs G-lane
+    rows (the narrow kernel, each row's shard range between two offset arrays), F = 50 two-line
+    rows on a wavefront each.  3 ranks sharing the GPU (gloo), overlap on (so pipelined),
+    dropout; each rank's block against the float64 oracle."""
+    env = dict(os.environ, PPNP_DIST_BACKEND="gloo", PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=3",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.join(ROOT, "tests", "dist_worker.py"), "--layout", "row", "--graph-n",
+           "200000", "--graph-m", "1000000", "--f", str(f), "--K", "3", "--oracle", "--overlap",
+           "--p-drop", "0.2"]
+    proc = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=150)
+    assert proc.returncode == 0, proc.stdout[-3000:] + proc.stderr[-3000:]
+    assert _rank_results(proc.stdout, "dist_worker") == {r: "OK" for r in range(3)}, \
+        proc.stdout[-4000:]
+    assert proc.stdout.count("pipeline=True") == 3, proc.stdout[-4000:]
+
+
 @pytest.mark.parametrize("ranks,extra", [(2, []), (2, ["--overlap"]),
                                          (3, ["--overlap", "--p-drop", "0.3"])])
 def test_row_partition_split_rows_matches_oracle(ranks, extra):
